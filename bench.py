@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s + fps of the CSG path tracer at 1920x1080, 64 spp,
+8 bounces on the 32-primitive CSG scene (BASELINE.json metric, config C3), on
+1..8 MI355X of one node.
+
+One process per GPU (torchrun).  Every rank renders its row-cyclic tiles of the
+SAME frame (strong scaling: the frame is fixed, rows are split), then the tiles
+are gathered to rank 0 over RCCL (torch.distributed "nccl") and un-interleaved by
+a HIP kernel.  A step = one full frame including the gather.
+
+    python bench.py                       # N=1, defaults finish in about a minute
+    torchrun --nproc-per-node 8 bench.py --gpus 8
+
+Prints ONE JSON line on rank 0.  `value` = traced ray segments of the whole frame
+(all ranks) / max-over-ranks wall time of the timed steps.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mrays/s + fps at 1920x1080x64spp, 32-prim CSG, 1/2/4/8 MI355X"
+# /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
+PEAK_FP32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scene", default="csg32",
+                    choices=["csg32", "rtiow_cover", "csg256_balanced", "csg256_chain", "sphere256"])
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--tile-rows", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the cpu_baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-json", default=None,
+                    help="per-dispatch HBM bytes measured by rocprofv3 --pmc (profiles/*.json) for roofline.traffic")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from csgrenderer_amd import scenes
+    from csgrenderer_amd import wololo as wl
+
+    r = wl.Renderer(f"bench{rank}", max_nodes=4096)
+    if args.scene == "sphere256":
+        info = scenes.sphere256()
+    else:
+        info = scenes.build(args.scene, r)
+    over = {"max_depth": args.depth}
+    if args.width:
+        over["width"] = args.width
+    if args.height:
+        over["height"] = args.height
+    if args.spp:
+        over["spp"] = args.spp
+    params = info.params(**over)
+    W, H, T = params.width, params.height, args.tile_rows
+    lr = wl.local_rows(H, T, world)
+    out = torch.empty((lr, W, 4), dtype=torch.float32, device=dev)
+    seg = torch.zeros(1, dtype=torch.int64, device=dev)
+    gathered = frame = None
+    if world > 1 and rank == 0:
+        gathered = [torch.empty((lr, W, 4), dtype=torch.float32, device=dev) for _ in range(world)]
+        frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    k_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            k_start[i].record(stream)
+        r.render_rows_device(params, out.data_ptr(), T, rank, world, sh, seg.data_ptr())
+        if i is not None:
+            k_end[i].record(stream)
+        if world > 1:
+            if rank == 0:
+                dist.gather(out, gather_list=gathered, dst=0)
+                stacked = torch.stack(gathered)  # rank-major [N, lr, W, 4]
+                wl.assemble_rows_device(stacked.data_ptr(), frame.data_ptr(), W, H, T, world, sh)
+            else:
+                dist.gather(out, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    seg.zero_()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    segs_total = seg.clone()
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(segs_total, op=dist.ReduceOp.SUM)
+    elapsed_s = float(elapsed.item())
+    segs_local = int(seg.item())
+    segs_all = int(segs_total.item())
+    k_ms = sum(k_start[i].elapsed_time(k_end[i]) for i in range(args.steps)) / args.steps
+
+    if rank == 0:
+        steps = args.steps
+        ms_per_step = elapsed_s / steps * 1e3
+        samples = W * H * (params.spp if info.mode == wl.MODE_PATHTRACE else 1)
+        if info.mode == wl.MODE_PATHTRACE:
+            value = segs_all / elapsed_s / 1e6
+            flop_launch = (segs_local / steps) * info.flop_per_segment
+            achieved_tf = flop_launch / (k_ms * 1e-3) / 1e12
+            roof = {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                    "kernel": "pathtrace_kernel", "kernel_ms": round(k_ms, 4),
+                    "flop_per_segment": info.flop_per_segment,
+                    "segments_per_launch": segs_local // steps}
+        else:
+            value = W * H * steps / elapsed_s / 1e6
+            bytes_launch = lr * W * 16
+            achieved = bytes_launch / (k_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": None, "kernel": "ubershader_kernel",
+                    "kernel_ms": round(k_ms, 5)}
+        # the store stream (16 B/pixel) against HBM, for the record
+        hbm_gbs = lr * W * 16 / (k_ms * 1e-3) / 1e9
+        if args.pmc_json and os.path.exists(args.pmc_json):
+            try:
+                pmc = json.load(open(args.pmc_json))
+                key = f"{args.scene}:{W}x{H}:{params.spp}:{world}"
+                if key in pmc:
+                    roof["traffic"] = pmc[key]
+            except Exception as e:  # report, don't fail the bench
+                print(f"[bench] pmc json unreadable: {e}", file=sys.stderr)
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline and info.mode == wl.MODE_PATHTRACE:
+            cpu = cpu_baseline(r, params, args.cpu_seconds)
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{info.name}: {W}x{H}, {params.spp} spp, {params.max_depth} bounces, "
+                                   f"{info.spheres} spheres + {info.halfspaces} half-spaces, {info.binops} binops",
+                       "scene": info.name, "width": W, "height": H, "spp": params.spp,
+                       "max_depth": params.max_depth, "tile_rows": T,
+                       "parallelism": f"row-cyclic tiles x{world}" + (" + RCCL gather" if world > 1 else "")},
+            "fps": round(steps / elapsed_s, 3),
+            "msamples_per_s": round(samples * steps / elapsed_s / 1e6, 3),
+            "segments_per_frame": segs_all // steps,
+            "roofline": roof,
+            "roofline_hbm_store": {"bound": "hbm", "achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS,
+                                   "unit": "GB/s", "frac": round(hbm_gbs / PEAK_HBM_GBS, 6)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(r, params, budget_s: float):
+    """The CPU oracle (oracle/oracle.c, a scalar C restatement of the same path) on a
+    bounded sample of the same frame: whole rows from the middle of the image, as many
+    as fit the time budget, on the host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    nthreads = pyoracle.nthreads_default()
+    prog, nrec, _ = r.program()
+    mats, nm = r.materials()
+    fr = r.frame_desc(params)
+    row = params.height // 2
+    rows = 0
+    segs = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s and row < params.height:
+        n = min(nthreads // 4 + 1, params.height - row)
+        _, s = pyoracle.pathtrace_rows(prog, nrec, mats, nm, fr, row, n, nthreads=nthreads)
+        segs += s
+        rows += n
+        row += n
+    dt = time.perf_counter() - t0
+    return {"value": round(segs / dt / 1e6, 4), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
+            "sample": f"rows {params.height // 2}..{params.height // 2 + rows - 1} ({rows} of {params.height}) of the "
+                      f"same {params.width}x{params.height} frame, {params.spp} spp, {params.max_depth} bounces; "
+                      f"{segs} segments in {dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

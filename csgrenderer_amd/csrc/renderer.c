@@ -1,0 +1,444 @@
+/*
+ * renderer.c -- the wololo renderer C API on HIP.
+ *
+ * Replaces src/wololo/renderer/renderer.c of the reference:
+ *   - node store: same semantics as allocate_node / set_nonroot_node /
+ *     add_*_node / wo_renderer_isroot (ref renderer.c:2220-2313), but the node
+ *     is allocated OUTSIDE assert() (the reference's allocation vanishes under
+ *     NDEBUG, renderer.c:2234) and a full store returns WO_NODE_INVALID;
+ *   - Vulkan init (renderer.c:394-1810) -> one WoDev (HIP device + stream);
+ *   - draw_frame_with_renderer (renderer.c:2085-2219): UBO {time, W, H} ->
+ *     WoFrame, vkQueueSubmit -> kernel launch, present -> optional image dump.
+ */
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "wo_internal.h"
+
+static _Thread_local char g_err[512];
+
+void wo_set_error(char const* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+
+char const* wo_renderer_last_error(void) { return g_err; }
+
+char const* wo_version(void) { return "wololo-mi355x 0.1 (gfx950)"; }
+
+double wo_monotonic_sec(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+int wo_hip_device_count(void) { return wo_dev_count(); }
+
+void wo_render_params_default(Wo_RenderParams* p) {
+    memset(p, 0, sizeof *p);
+    p->width = 1280;
+    p->height = 720;
+    p->spp = 1;
+    p->max_depth = 8;
+    p->seed = 0;
+    p->mode = WO_SHADING_UBERSHADER_RT1;
+    p->sample_offset = 0;
+    p->time_sec = 0.0f;
+}
+
+static int env_flag(const char* name) {
+    const char* v = getenv(name);
+    return v && *v && strcmp(v, "0") != 0;
+}
+
+/* ---------------------------------------------------------------- lifecycle */
+
+Wo_Renderer* wo_renderer_new(Wo_App* app, char const* name, size_t max_node_count) {
+    Wo_Renderer* r = (Wo_Renderer*)calloc(1, sizeof(Wo_Renderer));
+    if (!r) {
+        fprintf(stderr, WO_LOG_PREFIX " Failed to allocate Wo_Renderer.\n");
+        return NULL;
+    }
+    r->max_node_count = max_node_count;
+    size_t words = max_node_count / 64 + 1;
+    r->nodes = (WoNodeInfo*)calloc(max_node_count ? max_node_count : 1, sizeof(WoNodeInfo));
+    r->nonroot = (uint64_t*)calloc(words, sizeof(uint64_t));
+    r->cap_mats = 16;
+    r->mats = (WoMaterial*)calloc(r->cap_mats, sizeof(WoMaterial));
+    if (!r->nodes || !r->nonroot || !r->mats) {
+        fprintf(stderr, WO_LOG_PREFIX " Failed to allocate node tables for %zu nodes.\n", max_node_count);
+        wo_renderer_del(r);
+        return NULL;
+    }
+    /* name: copied; empty -> NULL (ref allocate_renderer, renderer.c:344-351, 384-391) */
+    if (name && name[0]) {
+        size_t n = strlen(name);
+        r->name = (char*)malloc(n + 1);
+        if (r->name) memcpy(r->name, name, n + 1);
+    }
+    r->app = app;
+    /* material 0: default lambertian grey */
+    r->mats[0].kind = WO_MAT_LAMBERTIAN;
+    r->mats[0].albedo[0] = r->mats[0].albedo[1] = r->mats[0].albedo[2] = 0.5f;
+    r->n_mats = 1;
+    r->camera.look_from = wo_vec3_make(0.0, 0.0, 0.0);
+    r->camera.look_at = wo_vec3_make(0.0, 0.0, -1.0);
+    r->camera.view_up = wo_vec3_make(0.0, 1.0, 0.0);
+    r->camera.vfov_deg = 90.0;
+    r->camera.aperture = 0.0;
+    r->camera.focus_dist = 1.0;
+    wo_render_params_default(&r->draw);
+    if (app) {
+        r->draw.width = wo_app_window_width(app);
+        r->draw.height = wo_app_window_height(app);
+    }
+    r->t0 = wo_monotonic_sec();
+    r->dirty = 1;
+    r->device = -1;
+
+    char err[256] = {0};
+    int ndev = wo_dev_count();
+    if (ndev <= 0) {
+        if (env_flag("WOLOLO_ALLOW_NO_DEVICE")) {
+            /* node store only (host tests); every render call fails loudly */
+            return r;
+        }
+        fprintf(stderr, WO_LOG_PREFIX " No HIP device available; cannot create renderer.\n");
+        wo_set_error("no HIP device available");
+        wo_renderer_del(r);
+        return NULL;
+    }
+    int dev = wo_dev_current();
+    if (dev < 0) dev = 0;
+    if (wo_dev_create(dev, &r->dev, err, sizeof err) != 0) {
+        fprintf(stderr, WO_LOG_PREFIX " HIP init failed: %s\n", err);
+        wo_set_error("HIP init failed: %s", err);
+        wo_renderer_del(r);
+        return NULL;
+    }
+    r->device = dev;
+    return r;
+}
+
+void wo_renderer_del(Wo_Renderer* r) {
+    if (!r) return;
+    if (r->dev) wo_dev_destroy(r->dev);
+    free(r->nodes);
+    free(r->nonroot);
+    free(r->mats);
+    free(r->prog);
+    free(r->host_frame);
+    free(r->name);
+    free(r);
+}
+
+/* ---------------------------------------------------------------- node store */
+
+static Wo_Node alloc_node(Wo_Renderer* r, uint32_t kind) {
+    if (r->node_count >= r->max_node_count) {
+        fprintf(stderr, WO_LOG_PREFIX " Failed to allocate a new renderer node -- the store holds %zu nodes.\n",
+                r->max_node_count);
+        wo_set_error("node store full (%zu nodes)", r->max_node_count);
+        return WO_NODE_INVALID;
+    }
+    Wo_Node n = (Wo_Node)r->node_count++;
+    memset(&r->nodes[n], 0, sizeof(WoNodeInfo));
+    r->nodes[n].kind = kind;
+    r->nodes[n].material = 0;
+    r->dirty = 1;
+    return n;
+}
+
+static void set_nonroot(Wo_Renderer* r, Wo_Node n) {
+    if (n < r->max_node_count) r->nonroot[n / 64] |= 1ull << (n % 64);
+}
+
+Wo_Node wo_renderer_add_sphere_node(Wo_Renderer* r, Wo_Scalar radius) {
+    Wo_Node n = alloc_node(r, WO_NODE_SPHERE);
+    if (n != WO_NODE_INVALID) r->nodes[n].radius = radius;
+    return n;
+}
+
+Wo_Node wo_renderer_add_infinite_planar_partition_node(Wo_Renderer* r, Wo_Vec3 outward_facing_normal) {
+    Wo_Node n = alloc_node(r, WO_NODE_HALFSPACE);
+    if (n != WO_NODE_INVALID) r->nodes[n].normal = outward_facing_normal;
+    return n;
+}
+
+static Wo_Node add_binop(Wo_Renderer* r, uint32_t kind, Wo_Node_Argument left, Wo_Node_Argument right) {
+    if (left.node >= r->node_count || right.node >= r->node_count) {
+        fprintf(stderr, WO_LOG_PREFIX " binop operand refers to an unknown node (%u, %u of %zu).\n", left.node,
+                right.node, r->node_count);
+        wo_set_error("binop operand refers to an unknown node");
+        return WO_NODE_INVALID;
+    }
+    Wo_Node n = alloc_node(r, kind);
+    if (n == WO_NODE_INVALID) return n;
+    r->nodes[n].left = left;
+    r->nodes[n].right = right;
+    set_nonroot(r, left.node);
+    set_nonroot(r, right.node);
+    return n;
+}
+
+Wo_Node wo_renderer_add_union_of_node(Wo_Renderer* r, Wo_Node_Argument left, Wo_Node_Argument right) {
+    return add_binop(r, WO_NODE_UNION, left, right);
+}
+
+Wo_Node wo_renderer_add_intersection_of_node(Wo_Renderer* r, Wo_Node_Argument left, Wo_Node_Argument right) {
+    return add_binop(r, WO_NODE_INTERSECTION, left, right);
+}
+
+Wo_Node wo_renderer_add_difference_of_node(Wo_Renderer* r, Wo_Node_Argument left, Wo_Node_Argument right) {
+    return add_binop(r, WO_NODE_DIFFERENCE, left, right);
+}
+
+bool wo_renderer_isroot(Wo_Renderer* r, Wo_Node node) {
+    if (node >= r->max_node_count) return false;
+    return (r->nonroot[node / 64] & (1ull << (node % 64))) == 0;
+}
+
+size_t wo_renderer_node_count(Wo_Renderer* r) { return r->node_count; }
+char const* wo_renderer_name(Wo_Renderer* r) { return r->name; }
+int wo_renderer_device(Wo_Renderer* r) { return r->device; }
+
+/* ---------------------------------------------------------------- materials */
+
+static Wo_Material add_material(Wo_Renderer* r, WoMaterial const* m) {
+    if (r->n_mats == r->cap_mats) {
+        uint32_t nc = r->cap_mats * 2u;
+        WoMaterial* nm = (WoMaterial*)realloc(r->mats, nc * sizeof(WoMaterial));
+        if (!nm) {
+            wo_set_error("out of host memory");
+            return WO_MATERIAL_INVALID;
+        }
+        r->mats = nm;
+        r->cap_mats = nc;
+    }
+    r->mats[r->n_mats] = *m;
+    r->dirty = 1;
+    return r->n_mats++;
+}
+
+Wo_Material wo_renderer_add_lambertian_material(Wo_Renderer* r, Wo_Vec3 albedo) {
+    WoMaterial m;
+    memset(&m, 0, sizeof m);
+    m.kind = WO_MAT_LAMBERTIAN;
+    m.albedo[0] = (float)albedo.x;
+    m.albedo[1] = (float)albedo.y;
+    m.albedo[2] = (float)albedo.z;
+    return add_material(r, &m);
+}
+
+Wo_Material wo_renderer_add_metal_material(Wo_Renderer* r, Wo_Vec3 albedo, Wo_Scalar fuzz) {
+    WoMaterial m;
+    memset(&m, 0, sizeof m);
+    m.kind = WO_MAT_METAL;
+    m.albedo[0] = (float)albedo.x;
+    m.albedo[1] = (float)albedo.y;
+    m.albedo[2] = (float)albedo.z;
+    m.fuzz = (float)(fuzz < 1.0 ? (fuzz > 0.0 ? fuzz : 0.0) : 1.0);
+    return add_material(r, &m);
+}
+
+Wo_Material wo_renderer_add_dielectric_material(Wo_Renderer* r, Wo_Scalar refraction_index) {
+    WoMaterial m;
+    memset(&m, 0, sizeof m);
+    m.kind = WO_MAT_DIELECTRIC;
+    m.albedo[0] = m.albedo[1] = m.albedo[2] = 1.0f;
+    m.ior = (float)refraction_index;
+    return add_material(r, &m);
+}
+
+bool wo_renderer_set_node_material(Wo_Renderer* r, Wo_Node leaf, Wo_Material material) {
+    if (leaf >= r->node_count || material >= r->n_mats) return false;
+    uint32_t k = r->nodes[leaf].kind;
+    if (k != WO_NODE_SPHERE && k != WO_NODE_HALFSPACE) return false;
+    r->nodes[leaf].material = material;
+    r->dirty = 1;
+    return true;
+}
+
+void wo_renderer_set_camera(Wo_Renderer* r, Wo_Vec3 look_from, Wo_Vec3 look_at, Wo_Vec3 view_up,
+                            Wo_Scalar vertical_fov_deg, Wo_Scalar aperture, Wo_Scalar focus_dist) {
+    r->camera.look_from = look_from;
+    r->camera.look_at = look_at;
+    r->camera.view_up = view_up;
+    r->camera.vfov_deg = vertical_fov_deg;
+    r->camera.aperture = aperture;
+    r->camera.focus_dist = focus_dist;
+}
+
+void wo_renderer_set_draw_params(Wo_Renderer* r, Wo_RenderParams const* params, int pin_time) {
+    r->draw = *params;
+    r->pin_time = pin_time;
+}
+
+/* ---------------------------------------------------------------- compile / frame */
+
+int wo_renderer_compile(Wo_Renderer* r) {
+    if (r->dirty || !r->prog) {
+        char err[256] = {0};
+        if (wo_compile_scene(r, err, sizeof err) != 0) {
+            wo_set_error("scene compile failed: %s", err);
+            return -1;
+        }
+    }
+    return (int)r->n_recs;
+}
+
+WoRec const* wo_renderer_program(Wo_Renderer* r, uint32_t* n_recs, uint32_t* n_prims) {
+    if (wo_renderer_compile(r) < 0) return NULL;
+    if (n_recs) *n_recs = r->n_recs;
+    if (n_prims) *n_prims = r->n_prims;
+    return r->prog;
+}
+
+WoMaterial const* wo_renderer_materials(Wo_Renderer* r, uint32_t* n_materials) {
+    if (n_materials) *n_materials = r->n_mats;
+    return r->mats;
+}
+
+/* Host float -> the ubershader's sphere height: amplitude * sin(omega * time),
+ * omega = fp32(2 * 3.1415 / 4) = 0x3fc90e56 (ubershader1.frag:101-103, folded). */
+static float ubershader_sphere_y(float time_sec) {
+    const float omega = 1.57075f;
+    return 2.0f * sinf(omega * time_sec);
+}
+
+int wo_renderer_frame_desc(Wo_Renderer* r, Wo_RenderParams const* p, uint32_t tile_rows, uint32_t rank,
+                           uint32_t nranks, WoFrame* out) {
+    if (wo_renderer_compile(r) < 0) return -1;
+    memset(out, 0, sizeof *out);
+    out->width = p->width;
+    out->height = p->height;
+    out->spp = p->spp;
+    out->max_depth = p->max_depth;
+    out->seed = p->seed;
+    out->mode = p->mode;
+    out->sample_offset = p->sample_offset;
+    out->tile_rows = tile_rows;
+    out->rank = rank;
+    out->nranks = nranks;
+    out->n_recs = r->n_recs;
+    out->n_prims = r->n_prims;
+    out->time_sec = p->time_sec;
+    out->sphere_y = ubershader_sphere_y(p->time_sec);
+    wo_resolve_camera(&r->camera, p->width, p->height, &out->cam);
+    return 0;
+}
+
+static int sync_device(Wo_Renderer* r) {
+    if (!r->dev) {
+        wo_set_error("renderer has no HIP device (created with WOLOLO_ALLOW_NO_DEVICE)");
+        fprintf(stderr, WO_LOG_PREFIX " render called on a device-less renderer.\n");
+        return -1;
+    }
+    if (wo_renderer_compile(r) < 0) return -1;
+    if (r->dev_stale) {
+        char err[256] = {0};
+        if (wo_dev_upload_scene(r->dev, r->prog, r->n_recs, r->n_prims, r->mats, r->n_mats, err, sizeof err)) {
+            wo_set_error("scene upload failed: %s", err);
+            return -1;
+        }
+        r->dev_stale = 0;
+    }
+    return 0;
+}
+
+int wo_renderer_render_f32(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba) {
+    if (sync_device(r)) return -1;
+    WoFrame fr;
+    if (wo_renderer_frame_desc(r, params, 16, 0, 1, &fr)) return -1;
+    char err[256] = {0};
+    if (wo_dev_render_host(r->dev, &fr, out_rgba, err, sizeof err)) {
+        wo_set_error("render failed: %s", err);
+        return -1;
+    }
+    return 0;
+}
+
+int wo_renderer_render_rows_device(Wo_Renderer* r, Wo_RenderParams const* params, void* d_out, uint32_t tile_rows,
+                                   uint32_t rank, uint32_t nranks, void* stream,
+                                   unsigned long long* d_segment_counter) {
+    if (sync_device(r)) return -1;
+    WoFrame fr;
+    if (wo_renderer_frame_desc(r, params, tile_rows, rank, nranks, &fr)) return -1;
+    char err[256] = {0};
+    if (wo_dev_launch(r->dev, &fr, d_out, stream, d_segment_counter, err, sizeof err)) {
+        wo_set_error("launch failed: %s", err);
+        return -1;
+    }
+    return 0;
+}
+
+int wo_assemble_rows_device(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,
+                            uint32_t tile_rows, uint32_t nranks, void* stream) {
+    char err[256] = {0};
+    if (wo_dev_assemble(d_gathered, d_frame, width, height, tile_rows, nranks, stream, err, sizeof err)) {
+        wo_set_error("%s", err);
+        return -1;
+    }
+    return 0;
+}
+
+/* ---------------------------------------------------------------- draw_frame */
+
+/* Present path, headless: the float framebuffer is clamped, sRGB-encoded (the
+ * reference's preferred B8G8R8A8_SRGB swapchain, renderer.c:819-831) and, when
+ * WOLOLO_OUTPUT names a file, written as a binary PPM. */
+static unsigned char srgb8(float v) {
+    if (!(v > 0.0f)) return 0;
+    if (v >= 1.0f) return 255;
+    float s = v <= 0.0031308f ? 12.92f * v : 1.055f * powf(v, 1.0f / 2.4f) - 0.055f;
+    int q = (int)(s * 255.0f + 0.5f);
+    return (unsigned char)(q < 0 ? 0 : q > 255 ? 255 : q);
+}
+
+static void write_ppm(const char* path, const float* rgba, uint32_t w, uint32_t h) {
+    FILE* f = fopen(path, "wb");
+    if (!f) {
+        fprintf(stderr, WO_LOG_PREFIX " cannot write %s\n", path);
+        return;
+    }
+    fprintf(f, "P6\n%u %u\n255\n", w, h);
+    unsigned char* row = (unsigned char*)malloc((size_t)w * 3);
+    if (row) {
+        for (uint32_t y = 0; y < h; ++y) {
+            for (uint32_t x = 0; x < w; ++x)
+                for (int c = 0; c < 3; ++c) row[x * 3 + c] = srgb8(rgba[((size_t)y * w + x) * 4 + c]);
+            fwrite(row, 1, (size_t)w * 3, f);
+        }
+        free(row);
+    }
+    fclose(f);
+}
+
+void wo_renderer_draw_frame(Wo_Renderer* r) {
+    if (!r) return;
+    Wo_RenderParams p = r->draw;
+    if (!r->pin_time) p.time_sec = (float)(r->app ? wo_app_time_sec(r->app) : wo_monotonic_sec() - r->t0);
+    size_t need = (size_t)p.width * p.height * 4;
+    if (need > r->host_frame_cap) {
+        free(r->host_frame);
+        r->host_frame = (float*)malloc(need * sizeof(float));
+        r->host_frame_cap = r->host_frame ? need : 0;
+        if (!r->host_frame) {
+            fprintf(stderr, WO_LOG_PREFIX " out of host memory for the framebuffer\n");
+            return;
+        }
+    }
+    if (wo_renderer_render_f32(r, &p, r->host_frame) != 0) {
+        fprintf(stderr, WO_LOG_PREFIX " draw_frame failed: %s\n", wo_renderer_last_error());
+        return;
+    }
+    r->frames_drawn++;
+    const char* out = getenv("WOLOLO_OUTPUT");
+    if (out && *out) write_ppm(out, r->host_frame, p.width, p.height);
+}

@@ -1,0 +1,82 @@
+/*
+ * wo_internal.h -- private structures of the host library.
+ *
+ * The node store mirrors the reference's (renderer.c:180-217): a type per node,
+ * a parameter record per node, and a non-root bitset; handles are sequential.
+ * The reference packs everything into one calloc slab (allocate_renderer,
+ * renderer.c:338-393); here the tables are separate allocations owned by the
+ * renderer, sized once from max_node_count.
+ */
+#ifndef WOLOLO_WO_INTERNAL_H
+#define WOLOLO_WO_INTERNAL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "wololo/config.h"
+#include "wololo/renderer/renderer_ext.h"
+#include "wololo/wo_scene.h"
+#include "wo_dev.h"
+
+/* Node kinds: same order as the reference's NodeType (renderer.c:182-188). */
+enum {
+    WO_NODE_SPHERE = 0,
+    WO_NODE_HALFSPACE = 1,
+    WO_NODE_UNION = 2,
+    WO_NODE_INTERSECTION = 3,
+    WO_NODE_DIFFERENCE = 4,
+};
+
+typedef struct WoNodeInfo {
+    uint32_t kind;
+    Wo_Material material;  /* leaves only */
+    Wo_Scalar radius;      /* sphere */
+    Wo_Vec3 normal;        /* half-space outward normal (as given) */
+    Wo_Node_Argument left, right;  /* binops */
+} WoNodeInfo;
+
+typedef struct WoCameraDesc {
+    Wo_Vec3 look_from, look_at, view_up;
+    double vfov_deg, aperture, focus_dist;
+} WoCameraDesc;
+
+struct Wo_Renderer {
+    size_t max_node_count;
+    size_t node_count;
+    WoNodeInfo* nodes;
+    uint64_t* nonroot;  /* bitset, ceil(max/64) words */
+    char* name;
+    Wo_App* app;
+
+    WoMaterial* mats;
+    uint32_t n_mats, cap_mats;
+
+    WoCameraDesc camera;
+
+    Wo_RenderParams draw;
+    int pin_time;
+    double t0;  /* creation time (seconds, monotonic) when there is no app */
+
+    /* compiled program (host copy) */
+    WoRec* prog;
+    uint32_t n_recs, n_prims, cap_recs;
+    int dirty;          /* nodes/materials changed since the last compile */
+    int dev_stale;      /* device copy out of date */
+
+    int device;         /* -1: device-less (tests only) */
+    WoDev* dev;
+
+    float* host_frame;
+    size_t host_frame_cap;
+    uint64_t frames_drawn;
+};
+
+/* scene_compile.c */
+int wo_compile_scene(Wo_Renderer* r, char* err, size_t errlen);
+void wo_resolve_camera(WoCameraDesc const* desc, uint32_t width, uint32_t height, WoCamera* out);
+
+/* renderer.c */
+void wo_set_error(char const* fmt, ...);
+double wo_monotonic_sec(void);
+
+#endif /* WOLOLO_WO_INTERNAL_H */

@@ -1,0 +1,281 @@
+"""Benchmark / parity scenes of BASELINE.json, built through the wololo node API.
+
+Every scene is constructed only with the reference's node calls
+(``wo_renderer_add_{sphere,infinite_planar_partition,union_of,intersection_of,
+difference_of}_node``, renderer.h:28-33) plus the material/camera extensions, so
+the same scene can be built from C.  Scene randomness uses PCG32 (O'Neill's
+pcg32_random_r, 64-bit LCG state, XSH-RR output) seeded as SURVEY.md §8(d) says:
+C2 0x5EED, C3 32, C5 256.
+
+Configs:
+  C1 sphere256   the reference shader, 256x256, 1 spp (no nodes needed)
+  C2 rtiow_cover RTIOW final scene, ~480 spheres as a balanced union tree
+  C3 csg32       32 leaves (20 spheres + 2 six-plane boxes), 31 binops, 63 nodes
+  C4 csg32_4k    C3 at 3840x2160, 256 spp (8-GPU row tiles)
+  C5 csg256      128 sphere leaves, 255 nodes: balanced tree or left-deep chain
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+from .wololo import (MODE_PATHTRACE, MODE_UBERSHADER_RT1, Renderer, arg, render_params)
+
+
+class Pcg32:
+    """pcg32_random_r with the default stream increment (seq 0x5851F42D... style)."""
+
+    MUL = 6364136223846793005
+    MASK = (1 << 64) - 1
+
+    def __init__(self, seed: int, seq: int = 0xDA3E39CB94B95BDB):
+        self.state = 0
+        self.inc = ((seq << 1) | 1) & self.MASK
+        self.next_u32()
+        self.state = (self.state + seed) & self.MASK
+        self.next_u32()
+
+    def next_u32(self) -> int:
+        old = self.state
+        self.state = (old * self.MUL + self.inc) & self.MASK
+        xorshifted = (((old >> 18) ^ old) >> 27) & 0xFFFFFFFF
+        rot = old >> 59
+        return ((xorshifted >> rot) | (xorshifted << ((-rot) & 31))) & 0xFFFFFFFF
+
+    def random(self) -> float:
+        """Uniform double in [0, 1) (32 random bits)."""
+        return self.next_u32() / 4294967296.0
+
+    def uniform(self, lo: float, hi: float) -> float:
+        return lo + (hi - lo) * self.random()
+
+
+@dataclass
+class SceneInfo:
+    name: str
+    spheres: int
+    halfspaces: int
+    binops: int
+    width: int
+    height: int
+    spp: int
+    max_depth: int
+    mode: int = MODE_PATHTRACE
+
+    @property
+    def leaves(self) -> int:
+        return self.spheres + self.halfspaces
+
+    @property
+    def flop_per_segment(self) -> int:
+        """30 per ray-sphere, 12 per ray-half-space, 4 per binop, 40 shading."""
+        return 30 * self.spheres + 12 * self.halfspaces + 4 * self.binops + 40
+
+    def params(self, **over):
+        kw = dict(width=self.width, height=self.height, spp=self.spp, max_depth=self.max_depth, mode=self.mode)
+        kw.update(over)
+        return render_params(**kw)
+
+
+def _balanced(r: Renderer, items, ops):
+    """items: list of (node, offset).  Returns (node, offset) of a balanced tree whose
+    internal nodes take their operator from ops() in creation order."""
+    if len(items) == 1:
+        return items[0]
+    h = len(items) // 2
+    ln, lo = _balanced(r, items[:h], ops)
+    rn, ro = _balanced(r, items[h:], ops)
+    op = ops()
+    n = {"u": r.union, "d": r.difference, "i": r.intersection}[op](arg(ln, lo), arg(rn, ro))
+    return n, (0.0, 0.0, 0.0)
+
+
+def _cycle(seq):
+    state = {"i": 0}
+
+    def nxt():
+        v = seq[state["i"] % len(seq)]
+        state["i"] += 1
+        return v
+
+    return nxt
+
+
+def _root(r: Renderer, item):
+    """A lone placed leaf cannot be a root (placement lives on binop operands):
+    wrap it as a union with itself."""
+    n, off = item
+    if off == (0.0, 0.0, 0.0):
+        return n
+    return r.union(arg(n, off), arg(n, off))
+
+
+def _random_material(r: Renderer, rng: Pcg32):
+    choose = rng.random()
+    if choose < 0.8:
+        return r.lambertian((rng.random() * rng.random(), rng.random() * rng.random(), rng.random() * rng.random()))
+    if choose < 0.95:
+        return r.metal((rng.uniform(0.5, 1), rng.uniform(0.5, 1), rng.uniform(0.5, 1)), rng.uniform(0, 0.5))
+    return r.dielectric(1.5)
+
+
+# ---------------------------------------------------------------------------------------------
+def sphere256() -> SceneInfo:
+    """C1: the reference path itself -- no scene nodes (ubershader1.frag ignores them)."""
+    return SceneInfo("sphere256", spheres=1, halfspaces=0, binops=0, width=256, height=256, spp=1, max_depth=1,
+                     mode=MODE_UBERSHADER_RT1)
+
+
+def build_rtiow_cover(r: Renderer, seed: int = 0x5EED) -> SceneInfo:
+    """C2: Ray Tracing in One Weekend's final scene (book 1, §13)."""
+    rng = Pcg32(seed)
+    items = []
+    ground = r.sphere(1000.0)
+    r.set_material(ground, r.lambertian((0.5, 0.5, 0.5)))
+    items.append((ground, (0.0, -1000.0, 0.0)))
+    for a in range(-11, 11):
+        for b in range(-11, 11):
+            choose = rng.random()
+            cx, cz = a + 0.9 * rng.random(), b + 0.9 * rng.random()
+            if math.sqrt((cx - 4.0) ** 2 + 0.0 + cz ** 2) <= 0.9:
+                continue
+            if choose < 0.8:
+                m = r.lambertian((rng.random() * rng.random(), rng.random() * rng.random(),
+                                  rng.random() * rng.random()))
+            elif choose < 0.95:
+                m = r.metal((rng.uniform(0.5, 1), rng.uniform(0.5, 1), rng.uniform(0.5, 1)), rng.uniform(0, 0.5))
+            else:
+                m = r.dielectric(1.5)
+            s = r.sphere(0.2)
+            r.set_material(s, m)
+            items.append((s, (cx, 0.2, cz)))
+    big = [((0.0, 1.0, 0.0), r.dielectric(1.5)), ((-4.0, 1.0, 0.0), r.lambertian((0.4, 0.2, 0.1))),
+           ((4.0, 1.0, 0.0), r.metal((0.7, 0.6, 0.5), 0.0))]
+    for c, m in big:
+        s = r.sphere(1.0)
+        r.set_material(s, m)
+        items.append((s, c))
+    n = len(items)
+    _root(r, _balanced(r, items, _cycle("u")))
+    r.set_camera((13, 2, 3), (0, 0, 0), (0, 1, 0), 20.0, 0.1, 10.0)
+    return SceneInfo("rtiow_cover", spheres=n, halfspaces=0, binops=n - 1, width=1920, height=1080, spp=64,
+                     max_depth=8)
+
+
+def _box(r: Renderer, center, half: float):
+    return _box_extents(r, center, (half, half, half))
+
+
+def _box_extents(r: Renderer, center, half):
+    """Axis-aligned box as a 6-half-space intersection chain (planes placed by offset)."""
+    normals = [(1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)]
+    planes = [(r.halfspace(n), tuple(c + h * k for c, h, k in zip(center, half, n))) for n in normals]
+    node, off = planes[0]
+    acc = None
+    for p, poff in planes[1:]:
+        if acc is None:
+            acc = r.intersection(arg(node, off), arg(p, poff))
+        else:
+            acc = r.intersection(arg(acc), arg(p, poff))
+    return acc, [p for p, _ in planes]
+
+
+def _overlapping_pairs(r: Renderer, rng: Pcg32, n_pairs: int, lo, hi, rmin: float, rmax: float, ops):
+    """n_pairs overlapping sphere pairs; pair k is combined with ops() so the CSG op
+    actually cuts (a lens, a bitten sphere or a blob).  Returns placed items."""
+    items = []
+    for _ in range(n_pairs):
+        ra = rng.uniform(rmin, rmax)
+        rb = rng.uniform(rmin, rmax)
+        ca = tuple(rng.uniform(a, b) for a, b in zip(lo, hi))
+        # second centre at 0.6..0.9 of the radius sum in a random direction
+        th, ph = rng.uniform(0, 2 * math.pi), math.acos(rng.uniform(-1, 1))
+        dist = rng.uniform(0.6, 0.9) * (ra + rb) * 0.75
+        cb = (ca[0] + dist * math.sin(ph) * math.cos(th), ca[1] + dist * math.cos(ph),
+              ca[2] + dist * math.sin(ph) * math.sin(th))
+        sa, sb = r.sphere(ra), r.sphere(rb)
+        r.set_material(sa, _random_material(r, rng))
+        r.set_material(sb, _random_material(r, rng))
+        op = {"u": r.union, "d": r.difference, "i": r.intersection}[ops()]
+        items.append((op(arg(sa, ca), arg(sb, cb)), (0.0, 0.0, 0.0)))
+    return items
+
+
+def build_csg32(r: Renderer, seed: int = 32, width=1920, height=1080, spp=64) -> SceneInfo:
+    """C3: 32 leaves (20 spheres + 12 half-spaces), 31 binops, 63 nodes.
+
+    Box A is a 12 x 0.5 x 12 floor slab (y in [-0.5, 0]) minus sphere0 (a crater);
+    box B a 1.5-unit cube intersected with sphere1 (a rounded cube); the other 18
+    spheres form 9 overlapping pairs whose ops cycle union / difference /
+    intersection, joined by a balanced union.  (SURVEY.md §8(d) sketches C3 with two
+    small boxes; the slab keeps the leaf/binop counts and gives the paths a floor
+    to bounce off.)"""
+    rng = Pcg32(seed)
+    slab, planes_a = _box_extents(r, (0.0, -0.25, 0.0), (6.0, 0.25, 6.0))
+    cube, planes_b = _box(r, (-2.0, 0.75, 0.0), 0.75)
+    ma, mb = r.lambertian((0.5, 0.5, 0.5)), r.metal((0.8, 0.8, 0.9), 0.05)
+    for p in planes_a:
+        r.set_material(p, ma)
+    for p in planes_b:
+        r.set_material(p, mb)
+    s0, s1 = r.sphere(1.2), r.sphere(1.0)
+    r.set_material(s0, r.lambertian((0.7, 0.3, 0.2)))
+    r.set_material(s1, r.metal((0.9, 0.8, 0.5), 0.1))
+    crater = r.difference(arg(slab), arg(s0, (2.5, 0.3, 1.5)))
+    rounded = r.intersection(arg(cube), arg(s1, (-2.0, 0.75, 0.0)))
+    pairs = _overlapping_pairs(r, rng, 9, (-4.0, 0.5, -4.0), (4.0, 2.0, 4.0), 0.3, 0.8, _cycle("udi"))
+    rest, roff = _balanced(r, pairs, _cycle("u"))
+    objs = r.union(arg(crater), arg(rounded))
+    r.union(arg(objs), arg(rest, roff))
+    r.set_camera((0.0, 4.5, 10.0), (0.0, 0.6, 0.0), (0, 1, 0), 45.0, 0.0, 10.0)
+    return SceneInfo("csg32", spheres=20, halfspaces=12, binops=31, width=width, height=height, spp=spp,
+                     max_depth=8)
+
+
+def build_csg256(r: Renderer, seed: int = 256, shape: str = "balanced", width=1920, height=1080,
+                 spp=64) -> SceneInfo:
+    """C5: 128 sphere leaves, 127 binops (255 nodes), leaf 0 an RTIOW-style ground
+    sphere (r = 1000).
+      balanced: 63 overlapping pairs (ops cycle u/d/i) + ground + 1 sphere, joined
+                by a balanced union;
+      chain:    a left-deep chain of depth 127 starting from the ground, ops cycling
+                u/u/d, so later spheres carve earlier ones and the ground."""
+    rng = Pcg32(seed)
+    ground = r.sphere(1000.0)
+    r.set_material(ground, r.lambertian((0.5, 0.5, 0.5)))
+    gitem = (ground, (0.0, -1000.0, 0.0))
+    if shape == "balanced":
+        items = [gitem] + _overlapping_pairs(r, rng, 63, (-5.0, 0.3, -5.0), (5.0, 2.5, 5.0), 0.25, 0.6,
+                                               _cycle("udi"))
+        s = r.sphere(1.0)
+        r.set_material(s, r.dielectric(1.5))
+        items.append((s, (0.0, 1.0, 0.0)))
+        _root(r, _balanced(r, items, _cycle("u")))
+    elif shape == "chain":
+        ops = _cycle("uud")
+        n, off = gitem
+        acc = None
+        for _ in range(127):
+            rad = rng.uniform(0.3, 0.7)
+            c = (rng.uniform(-4, 4), rng.uniform(0.0, 2.0), rng.uniform(-4, 4))
+            s = r.sphere(rad)
+            r.set_material(s, _random_material(r, rng))
+            op = {"u": r.union, "d": r.difference}[ops()]
+            acc = op(arg(n, off), arg(s, c)) if acc is None else op(arg(acc), arg(s, c))
+    else:
+        raise ValueError(shape)
+    r.set_camera((0.0, 6.0, 13.0), (0.0, 0.8, 0.0), (0, 1, 0), 45.0, 0.0, 13.0)
+    return SceneInfo(f"csg256_{shape}", spheres=128, halfspaces=0, binops=127, width=width, height=height, spp=spp,
+                     max_depth=8)
+
+
+SCENES = {
+    "rtiow_cover": build_rtiow_cover,
+    "csg32": build_csg32,
+    "csg256_balanced": lambda r, **k: build_csg256(r, shape="balanced", **k),
+    "csg256_chain": lambda r, **k: build_csg256(r, shape="chain", **k),
+}
+
+
+def build(name: str, r: Renderer, **kw) -> SceneInfo:
+    return SCENES[name](r, **kw)

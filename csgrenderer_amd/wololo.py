@@ -1,0 +1,292 @@
+"""ctypes mirror of the wololo C API (libwololo.so).
+
+The product is the C-ABI library built from ``csgrenderer_amd/csrc`` (HIP
+kernels for gfx950 + C host).  This module only binds it -- same names and
+argument meaning as the reference's ``src/wololo/renderer/renderer.h:18-33``
+and ``src/wololo/app.h:20-30`` plus the extensions of
+``include/wololo/renderer/renderer_ext.h`` -- so tests and ``bench.py`` read
+like C callers.  There is no fallback: if the library is missing, loading
+raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_bool, c_char_p, c_double, c_float, c_int, c_size_t, c_uint32,
+                    c_ulonglong, c_void_p)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libwololo.so")
+
+# ---- wo_scene.h constants -------------------------------------------------------------------
+WO_OP_PRIM, WO_OP_UNION, WO_OP_INTER, WO_OP_DIFF, WO_OP_RDIFF, WO_OP_BOUND = 1, 2, 3, 4, 5, 6
+WO_LEAF_SPHERE, WO_LEAF_HALFSPACE = 16, 17
+WO_MAT_LAMBERTIAN, WO_MAT_METAL, WO_MAT_DIELECTRIC = 0, 1, 2
+MODE_UBERSHADER_RT1, MODE_DEBUG_ST, MODE_PATHTRACE, MODE_NORMALS = 0, 1, 2, 3
+WO_T_MIN = 1.0e-3
+WO_NODE_INVALID = 0xFFFFFFFF
+
+
+class Vec3(Structure):
+    _fields_ = [("x", c_double), ("y", c_double), ("z", c_double)]
+
+
+class Quaternion(Structure):
+    _fields_ = [("real", c_double), ("imaginary", Vec3)]
+
+
+class NodeArgument(Structure):
+    _fields_ = [("orientation", Quaternion), ("offset", Vec3), ("node", c_uint32)]
+
+
+class RenderParams(Structure):
+    _fields_ = [("width", c_uint32), ("height", c_uint32), ("spp", c_uint32), ("max_depth", c_uint32),
+                ("seed", c_uint32), ("mode", c_uint32), ("sample_offset", c_uint32), ("time_sec", c_float)]
+
+
+class WoRec(Structure):
+    _fields_ = [("op", c_uint32), ("u0", c_uint32), ("u1", c_uint32), ("f", c_float * 5)]
+
+
+class WoMaterial(Structure):
+    _fields_ = [("kind", c_uint32), ("albedo", c_float * 3), ("fuzz", c_float), ("ior", c_float),
+                ("pad", c_float * 2)]
+
+
+class WoCamera(Structure):
+    _fields_ = [("origin", c_float * 3), ("lower_left", c_float * 3), ("horizontal", c_float * 3),
+                ("vertical", c_float * 3), ("u", c_float * 3), ("v", c_float * 3), ("lens_radius", c_float),
+                ("pad", c_float * 3)]
+
+
+class WoFrame(Structure):
+    _fields_ = [("width", c_uint32), ("height", c_uint32), ("spp", c_uint32), ("max_depth", c_uint32),
+                ("seed", c_uint32), ("mode", c_uint32), ("sample_offset", c_uint32), ("tile_rows", c_uint32),
+                ("rank", c_uint32), ("nranks", c_uint32), ("n_recs", c_uint32), ("n_prims", c_uint32),
+                ("time_sec", c_float), ("sphere_y", c_float), ("pad", c_float * 2), ("cam", WoCamera)]
+
+
+assert ctypes.sizeof(Vec3) == 24 and ctypes.sizeof(Quaternion) == 32 and ctypes.sizeof(NodeArgument) == 64
+assert ctypes.sizeof(WoRec) == 32 and ctypes.sizeof(WoMaterial) == 32
+
+# Every exported symbol and its signature (restype, argtypes).  tests/ check that the
+# library exports exactly these names (the C-ABI declared in include/wololo/*.h).
+_R = POINTER(ctypes.c_char)  # opaque Wo_Renderer*
+SIGNATURES = {
+    # renderer.h (reference API)
+    "wo_renderer_new": (c_void_p, [c_void_p, c_char_p, c_size_t]),
+    "wo_renderer_del": (None, [c_void_p]),
+    "wo_renderer_draw_frame": (None, [c_void_p]),
+    "wo_renderer_add_sphere_node": (c_uint32, [c_void_p, c_double]),
+    "wo_renderer_add_infinite_planar_partition_node": (c_uint32, [c_void_p, Vec3]),
+    "wo_renderer_add_union_of_node": (c_uint32, [c_void_p, NodeArgument, NodeArgument]),
+    "wo_renderer_add_intersection_of_node": (c_uint32, [c_void_p, NodeArgument, NodeArgument]),
+    "wo_renderer_add_difference_of_node": (c_uint32, [c_void_p, NodeArgument, NodeArgument]),
+    "wo_renderer_isroot": (c_bool, [c_void_p, c_uint32]),
+    # app.h (reference API + extensions)
+    "wo_app_new": (c_void_p, [c_double, c_uint32, c_uint32, c_char_p, c_void_p, c_void_p, c_void_p]),
+    "wo_app_run": (c_bool, [c_void_p]),
+    "wo_app_swap_scene": (None, [c_void_p, c_void_p]),
+    "wo_app_glfw_window": (c_void_p, [c_void_p]),
+    "wo_app_window_width": (c_uint32, [c_void_p]),
+    "wo_app_window_height": (c_uint32, [c_void_p]),
+    "wo_app_time_sec": (c_double, [c_void_p]),
+    # renderer_ext.h
+    "wo_render_params_default": (None, [POINTER(RenderParams)]),
+    "wo_renderer_add_lambertian_material": (c_uint32, [c_void_p, Vec3]),
+    "wo_renderer_add_metal_material": (c_uint32, [c_void_p, Vec3, c_double]),
+    "wo_renderer_add_dielectric_material": (c_uint32, [c_void_p, c_double]),
+    "wo_renderer_set_node_material": (c_bool, [c_void_p, c_uint32, c_uint32]),
+    "wo_renderer_set_camera": (None, [c_void_p, Vec3, Vec3, Vec3, c_double, c_double, c_double]),
+    "wo_renderer_set_draw_params": (None, [c_void_p, POINTER(RenderParams), c_int]),
+    "wo_renderer_render_f32": (c_int, [c_void_p, POINTER(RenderParams), c_void_p]),
+    "wo_renderer_render_rows_device": (c_int, [c_void_p, POINTER(RenderParams), c_void_p, c_uint32, c_uint32,
+                                               c_uint32, c_void_p, c_void_p]),
+    "wo_assemble_rows_device": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_void_p]),
+    "wo_renderer_compile": (c_int, [c_void_p]),
+    "wo_renderer_program": (POINTER(WoRec), [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
+    "wo_renderer_materials": (POINTER(WoMaterial), [c_void_p, POINTER(c_uint32)]),
+    "wo_renderer_frame_desc": (c_int, [c_void_p, POINTER(RenderParams), c_uint32, c_uint32, c_uint32,
+                                       POINTER(WoFrame)]),
+    "wo_renderer_node_count": (c_size_t, [c_void_p]),
+    "wo_renderer_name": (c_char_p, [c_void_p]),
+    "wo_renderer_device": (c_int, [c_void_p]),
+    "wo_renderer_last_error": (c_char_p, []),
+    "wo_version": (c_char_p, []),
+    "wo_hip_device_count": (c_int, []),
+}
+
+_lib = None
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load libwololo.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"libwololo.so not found at {p}; build it with `python -c 'import __graft_entry__ as g; "
+                           f"g.build()'` or `make -C csgrenderer_amd/csrc`")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def vec3(x, y, z) -> Vec3:
+    return Vec3(float(x), float(y), float(z))
+
+
+def quat_identity() -> Quaternion:
+    return Quaternion(1.0, Vec3(0.0, 0.0, 0.0))
+
+
+def arg(node: int, offset=(0.0, 0.0, 0.0), orientation: Quaternion | None = None) -> NodeArgument:
+    return NodeArgument(orientation or quat_identity(), vec3(*offset), int(node))
+
+
+def last_error() -> str:
+    e = load().wo_renderer_last_error()
+    return e.decode() if e else ""
+
+
+class WololoError(RuntimeError):
+    pass
+
+
+class Renderer:
+    """Thin owner of a Wo_Renderer* (all calls go straight to the C library)."""
+
+    def __init__(self, name: str = "py", max_nodes: int = 1024, app: int | None = None):
+        self.lib = load()
+        self.ptr = self.lib.wo_renderer_new(app, name.encode(), max_nodes)
+        if not self.ptr:
+            raise WololoError(f"wo_renderer_new failed: {last_error()}")
+
+    def close(self):
+        if self.ptr:
+            self.lib.wo_renderer_del(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- nodes (reference API) ----
+    def _check(self, n: int) -> int:
+        if n == WO_NODE_INVALID:
+            raise WololoError(last_error())
+        return n
+
+    def sphere(self, radius: float) -> int:
+        return self._check(self.lib.wo_renderer_add_sphere_node(self.ptr, float(radius)))
+
+    def halfspace(self, normal) -> int:
+        return self._check(self.lib.wo_renderer_add_infinite_planar_partition_node(self.ptr, vec3(*normal)))
+
+    def union(self, a: NodeArgument, b: NodeArgument) -> int:
+        return self._check(self.lib.wo_renderer_add_union_of_node(self.ptr, a, b))
+
+    def intersection(self, a: NodeArgument, b: NodeArgument) -> int:
+        return self._check(self.lib.wo_renderer_add_intersection_of_node(self.ptr, a, b))
+
+    def difference(self, a: NodeArgument, b: NodeArgument) -> int:
+        return self._check(self.lib.wo_renderer_add_difference_of_node(self.ptr, a, b))
+
+    def isroot(self, n: int) -> bool:
+        return bool(self.lib.wo_renderer_isroot(self.ptr, n))
+
+    # ---- extensions ----
+    def lambertian(self, albedo) -> int:
+        return self.lib.wo_renderer_add_lambertian_material(self.ptr, vec3(*albedo))
+
+    def metal(self, albedo, fuzz: float) -> int:
+        return self.lib.wo_renderer_add_metal_material(self.ptr, vec3(*albedo), float(fuzz))
+
+    def dielectric(self, ior: float) -> int:
+        return self.lib.wo_renderer_add_dielectric_material(self.ptr, float(ior))
+
+    def set_material(self, leaf: int, mat: int):
+        if not self.lib.wo_renderer_set_node_material(self.ptr, leaf, mat):
+            raise WololoError(f"set_node_material({leaf}, {mat}) rejected")
+
+    def set_camera(self, look_from, look_at, vup=(0, 1, 0), vfov=90.0, aperture=0.0, focus_dist=1.0):
+        self.lib.wo_renderer_set_camera(self.ptr, vec3(*look_from), vec3(*look_at), vec3(*vup), float(vfov),
+                                        float(aperture), float(focus_dist))
+
+    def compile(self) -> int:
+        n = self.lib.wo_renderer_compile(self.ptr)
+        if n < 0:
+            raise WololoError(last_error())
+        return n
+
+    def program(self):
+        """(records ctypes array, n_prims) of the compiled scene."""
+        nr, npr = c_uint32(0), c_uint32(0)
+        p = self.lib.wo_renderer_program(self.ptr, ctypes.byref(nr), ctypes.byref(npr))
+        if not p:
+            raise WololoError(last_error())
+        arr = (WoRec * max(nr.value, 1))()
+        if nr.value:
+            ctypes.memmove(arr, p, ctypes.sizeof(WoRec) * nr.value)
+        return arr, nr.value, npr.value
+
+    def materials(self):
+        n = c_uint32(0)
+        p = self.lib.wo_renderer_materials(self.ptr, ctypes.byref(n))
+        arr = (WoMaterial * max(n.value, 1))()
+        ctypes.memmove(arr, p, ctypes.sizeof(WoMaterial) * n.value)
+        return arr, n.value
+
+    def frame_desc(self, params: RenderParams, tile_rows=16, rank=0, nranks=1) -> WoFrame:
+        fr = WoFrame()
+        if self.lib.wo_renderer_frame_desc(self.ptr, ctypes.byref(params), tile_rows, rank, nranks,
+                                           ctypes.byref(fr)):
+            raise WololoError(last_error())
+        return fr
+
+    def render(self, params: RenderParams):
+        """Full frame to host; returns a float32 numpy array (H, W, 4)."""
+        import numpy as np
+        out = np.empty((params.height, params.width, 4), dtype=np.float32)
+        if self.lib.wo_renderer_render_f32(self.ptr, ctypes.byref(params), out.ctypes.data_as(c_void_p)):
+            raise WololoError(last_error())
+        return out
+
+    def render_rows_device(self, params: RenderParams, d_out: int, tile_rows: int, rank: int, nranks: int,
+                           stream: int = 0, d_segments: int = 0):
+        if self.lib.wo_renderer_render_rows_device(self.ptr, ctypes.byref(params), c_void_p(d_out), tile_rows, rank,
+                                                   nranks, c_void_p(stream or None),
+                                                   c_void_p(d_segments or None)):
+            raise WololoError(last_error())
+
+
+def render_params(width=256, height=256, spp=1, max_depth=8, seed=0, mode=MODE_UBERSHADER_RT1, sample_offset=0,
+                  time_sec=0.0) -> RenderParams:
+    return RenderParams(width, height, spp, max_depth, seed, mode, sample_offset, float(time_sec))
+
+
+def assemble_rows_device(d_gathered: int, d_frame: int, width: int, height: int, tile_rows: int, nranks: int,
+                         stream: int = 0):
+    lib = load()
+    if lib.wo_assemble_rows_device(c_void_p(d_gathered), c_void_p(d_frame), width, height, tile_rows, nranks,
+                                   c_void_p(stream or None)):
+        raise WololoError(last_error())
+
+
+def local_rows(height: int, tile_rows: int, nranks: int) -> int:
+    """Mirror of wo_rank_local_rows() (wo_scene.h)."""
+    tiles = (height + tile_rows - 1) // tile_rows
+    return ((tiles + nranks - 1) // nranks) * tile_rows
+
+
+def global_row(lrow: int, tile_rows: int, rank: int, nranks: int) -> int:
+    lt = lrow // tile_rows
+    return (lt * nranks + rank) * tile_rows + (lrow - lt * tile_rows)

@@ -1,0 +1,107 @@
+/*
+ * wololo/renderer/renderer_ext.h -- headless / north-star extensions of the
+ * renderer API.  New names only; nothing here changes renderer.h.
+ *
+ * The reference declares `Wo_Material` but never uses it (renderer.h:16) and has
+ * no camera, sample-count or bounce controls; its per-frame inputs are the 12-byte
+ * UBO {time, W, H} (renderer.c:72-80, 2133-2155).  These calls add them.
+ *
+ * Return convention for int-returning calls: 0 on success, negative on error;
+ * wo_renderer_last_error() returns a thread-local message for the last failure.
+ */
+#ifndef WOLOLO_RENDERER_RENDERER_EXT_H
+#define WOLOLO_RENDERER_RENDERER_EXT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "wololo/renderer/renderer.h"
+#include "wololo/wo_scene.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WO_NODE_INVALID ((Wo_Node)0xFFFFFFFFu)
+#define WO_MATERIAL_INVALID ((Wo_Material)0xFFFFFFFFu)
+
+typedef enum Wo_ShadingMode {
+    WO_SHADING_UBERSHADER_RT1 = WO_MODE_UBERSHADER_RT1, /* default: the reference's image */
+    WO_SHADING_DEBUG_ST = WO_MODE_DEBUG_ST,
+    WO_SHADING_PATHTRACE = WO_MODE_PATHTRACE,
+    WO_SHADING_NORMALS = WO_MODE_NORMALS,
+} Wo_ShadingMode;
+
+typedef struct Wo_RenderParams {
+    uint32_t width, height;  /* frame size in pixels */
+    uint32_t spp;            /* samples per pixel (PATHTRACE) */
+    uint32_t max_depth;      /* max segments per path (PATHTRACE) */
+    uint32_t seed;           /* RNG stream selector */
+    uint32_t mode;           /* Wo_ShadingMode */
+    uint32_t sample_offset;  /* index of the first sample (progressive rendering) */
+    float time_sec;          /* UBERSHADER_RT1: time_since_start_sec */
+} Wo_RenderParams;
+
+/* Defaults: 1280x720 (or the app window), 1 spp, 8 segments, seed 0, UBERSHADER_RT1. */
+void wo_render_params_default(Wo_RenderParams* params);
+
+/* ---- materials (leaf nodes carry one; the default, id 0, is lambertian 0.5 grey) ---- */
+Wo_Material wo_renderer_add_lambertian_material(Wo_Renderer* r, Wo_Vec3 albedo);
+Wo_Material wo_renderer_add_metal_material(Wo_Renderer* r, Wo_Vec3 albedo, Wo_Scalar fuzz);
+Wo_Material wo_renderer_add_dielectric_material(Wo_Renderer* r, Wo_Scalar refraction_index);
+/* Only sphere / half-space leaves take materials.  Returns false on a bad handle. */
+bool wo_renderer_set_node_material(Wo_Renderer* r, Wo_Node leaf, Wo_Material material);
+
+/* ---- camera (RTIOW "positionable camera" with defocus blur) ---- */
+void wo_renderer_set_camera(Wo_Renderer* r, Wo_Vec3 look_from, Wo_Vec3 look_at, Wo_Vec3 view_up,
+                            Wo_Scalar vertical_fov_deg, Wo_Scalar aperture, Wo_Scalar focus_dist);
+
+/* Parameters used by wo_renderer_draw_frame(); time_sec is overridden by the
+ * app clock unless `pin_time` is non-zero. */
+void wo_renderer_set_draw_params(Wo_Renderer* r, Wo_RenderParams const* params, int pin_time);
+
+/* Render a whole frame into a host buffer of width*height*4 floats (RGBA,
+ * row 0 = top).  Synchronous.  Includes the device->host copy. */
+int wo_renderer_render_f32(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba);
+
+/* Render this rank's row tiles into DEVICE memory `d_out`
+ * (wo_rank_local_rows(height, tile_rows, nranks) * width float4s) on HIP stream
+ * `stream` (NULL = default stream), asynchronously.  Tiles are `tile_rows` rows;
+ * rank r owns tiles g with g % nranks == r, stored in increasing g.  If
+ * `d_segment_counter` is non-NULL, the number of traced CSG ray segments is
+ * atomically added to it (uint64, device memory). */
+int wo_renderer_render_rows_device(Wo_Renderer* r, Wo_RenderParams const* params, void* d_out,
+                                   uint32_t tile_rows, uint32_t rank, uint32_t nranks, void* stream,
+                                   unsigned long long* d_segment_counter);
+
+/* Un-interleave nranks gathered local buffers (rank-major, each
+ * wo_rank_local_rows(...) * width float4s) into a width*height float4 frame. */
+int wo_assemble_rows_device(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,
+                            uint32_t tile_rows, uint32_t nranks, void* stream);
+
+/* Compile the node tables into the flattened program (done lazily by every
+ * render call; exposed for tests).  Returns the number of records. */
+int wo_renderer_compile(Wo_Renderer* r);
+/* Host views of the compiled scene (valid until the next node/material change). */
+WoRec const* wo_renderer_program(Wo_Renderer* r, uint32_t* n_recs, uint32_t* n_prims);
+WoMaterial const* wo_renderer_materials(Wo_Renderer* r, uint32_t* n_materials);
+/* Fill a WoFrame exactly as the kernels receive it (camera resolved for params). */
+int wo_renderer_frame_desc(Wo_Renderer* r, Wo_RenderParams const* params, uint32_t tile_rows,
+                           uint32_t rank, uint32_t nranks, WoFrame* out);
+
+size_t wo_renderer_node_count(Wo_Renderer* r);
+char const* wo_renderer_name(Wo_Renderer* r);
+/* HIP device ordinal the renderer runs on; -1 for a device-less renderer. */
+int wo_renderer_device(Wo_Renderer* r);
+char const* wo_renderer_last_error(void);
+
+/* ---- library-level ---- */
+char const* wo_version(void);
+/* Number of visible HIP devices (0 when none / no driver). */
+int wo_hip_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WOLOLO_RENDERER_RENDERER_EXT_H */

@@ -1,0 +1,126 @@
+/*
+ * wololo/wo_scene.h -- the flattened scene ("CSG program") and per-frame
+ * parameters as they sit in HBM / LDS.  This is a DATA contract: the host scene
+ * compiler (csgrenderer_amd/csrc/scene_compile.c) writes it, the HIP kernels
+ * (csrc/trace_kernels.hip) and the CPU oracle (oracle/oracle.c) read it.
+ *
+ * The reference never ships its node tables to the GPU: its
+ * host tables are NodeType + NodeInfo (renderer.c:180-202).  Here they are
+ * compiled into a postfix program over convex primitives:
+ *
+ *   WO_OP_PRIM   one convex primitive = intersection of `u0` member leaves,
+ *                followed by exactly u0 WoRec leaf records (WO_LEAF_*).
+ *                u1 = primitive ordinal (postfix order, dense from 0).
+ *   WO_OP_UNION / _INTER / _DIFF / _RDIFF   pop B (top), pop A, push
+ *                A|B, A&B, A&~B, B&~A.  (RDIFF lets the compiler emit the
+ *                subtrahend first to keep the evaluation stack shallow.)
+ *   WO_OP_BOUND  conservative bounding sphere (f[0..2] centre, f[3] R^2,
+ *                f[4] R) of the subtree that starts at the next record and
+ *                ends at record u0-1.  A kernel MAY skip that subtree (value =
+ *                empty set) when no ray of interest can touch the sphere; an
+ *                evaluator that ignores BOUND gets identical results.
+ *
+ * Every record is 32 bytes (8 dwords) so a wave reads one with two 16-byte
+ * LDS broadcasts or one scalar s_load_dwordx8.
+ */
+#ifndef WOLOLO_WO_SCENE_H
+#define WOLOLO_WO_SCENE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    WO_OP_PRIM = 1,
+    WO_OP_UNION = 2,
+    WO_OP_INTER = 3,
+    WO_OP_DIFF = 4,
+    WO_OP_RDIFF = 5,
+    WO_OP_BOUND = 6,
+};
+
+enum {
+    WO_LEAF_SPHERE = 16,     /* f: cx cy cz r^2 1/r */
+    WO_LEAF_HALFSPACE = 17,  /* f: nx ny nz h   ({x : n.x <= h}, |n| = 1) */
+};
+
+typedef struct WoRec {
+    uint32_t op;   /* WO_OP_* or WO_LEAF_* */
+    uint32_t u0;   /* PRIM: member count; BOUND: skip target; leaf: material id */
+    uint32_t u1;   /* PRIM: primitive ordinal */
+    float f[5];
+} WoRec;
+
+enum {
+    WO_MAT_LAMBERTIAN = 0,
+    WO_MAT_METAL = 1,
+    WO_MAT_DIELECTRIC = 2,
+};
+
+typedef struct WoMaterial {
+    uint32_t kind;
+    float albedo[3];
+    float fuzz;   /* metal */
+    float ior;    /* dielectric refraction index */
+    float pad[2];
+} WoMaterial;
+
+/* Shading modes (Wo_ShadingMode in renderer_ext.h uses the same values). */
+enum {
+    WO_MODE_UBERSHADER_RT1 = 0, /* reference ubershader1.frag ep_rt1_1 (animated sphere) */
+    WO_MODE_DEBUG_ST = 1,       /* reference ep_debug_view_1: (st.x, st.y, 0, 1) */
+    WO_MODE_PATHTRACE = 2,      /* CSG scene, materials, spp, bounces */
+    WO_MODE_NORMALS = 3,        /* CSG scene, 1 primary ray at the pixel centre, 0.5*(n+1) */
+};
+
+/* Camera already resolved to floats for one frame size (RTIOW camera model). */
+typedef struct WoCamera {
+    float origin[3];
+    float lower_left[3];
+    float horizontal[3];
+    float vertical[3];
+    float u[3];
+    float v[3];
+    float lens_radius;
+    float pad[3];
+} WoCamera;
+
+typedef struct WoFrame {
+    uint32_t width, height;     /* full frame */
+    uint32_t spp;               /* samples per pixel */
+    uint32_t max_depth;         /* max traced segments per path */
+    uint32_t seed;              /* frame seed */
+    uint32_t mode;              /* WO_MODE_* */
+    uint32_t sample_offset;     /* first sample index */
+    uint32_t tile_rows;         /* row-cyclic tiling: tile height in rows */
+    uint32_t rank, nranks;      /* this device renders tiles g with g % nranks == rank */
+    uint32_t n_recs;            /* program length */
+    uint32_t n_prims;           /* primitive count */
+    float time_sec;             /* ubershader: UBO time_since_start_sec */
+    float sphere_y;             /* ubershader: 2*sin(omega*time), hoisted to the host */
+    float pad[2];
+    WoCamera cam;
+} WoFrame;
+
+/* Minimum ray parameter for every CSG segment (RTIOW's 0.001). */
+#define WO_T_MIN (1.0e-3f)
+
+/* Number of tile rows a rank owns for a frame of `height` rows. */
+static inline uint32_t wo_rank_tile_count(uint32_t height, uint32_t tile_rows, uint32_t rank, uint32_t nranks) {
+    uint32_t tiles = (height + tile_rows - 1u) / tile_rows;
+    return rank < tiles ? (tiles - rank + nranks - 1u) / nranks : 0u;
+}
+
+/* Rows in one rank's local (gather) buffer: the same for every rank. */
+static inline uint32_t wo_rank_local_rows(uint32_t height, uint32_t tile_rows, uint32_t nranks) {
+    uint32_t tiles = (height + tile_rows - 1u) / tile_rows;
+    return ((tiles + nranks - 1u) / nranks) * tile_rows;
+}
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WOLOLO_WO_SCENE_H */

@@ -1,0 +1,238 @@
+"""GPU parity: HIP kernels (through the C-ABI of libwololo.so) vs the CPU oracle.
+
+Bar: bit-exact (max |delta| == 0) for every comparison below -- both sides are
+IEEE fp32 with the same op order, correctly rounded div/sqrt and no contraction.
+The north_star tolerance (1e-4 max per channel) is asserted as well so a
+failure message shows which bar broke.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+from csgrenderer_amd import scenes
+from csgrenderer_amd import wololo as wl
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TOL = 1e-4  # north_star: max per-channel |delta| < 1e-4
+
+
+def _cmp(gpu, ref, what):
+    gpu = np.asarray(gpu, dtype=np.float32)
+    ref = np.asarray(ref, dtype=np.float32)
+    assert gpu.shape == ref.shape, what
+    both_nan = np.isnan(gpu) & np.isnan(ref)
+    d = np.where(both_nan, 0.0, np.abs(gpu.astype(np.float64) - ref.astype(np.float64)))
+    mx = float(np.nanmax(d)) if d.size else 0.0
+    nbad = int((d > 0).sum())
+    assert mx < TOL, f"{what}: max |delta| {mx} >= {TOL} ({nbad} values differ)"
+    assert nbad == 0, f"{what}: not bit-exact ({nbad} values differ, max {mx})"
+
+
+@pytest.fixture(scope="module")
+def empty_renderer():
+    r = wl.Renderer("uber", max_nodes=8)
+    yield r
+    r.close()
+
+
+@pytest.mark.parametrize("w,h", [(256, 256), (1280, 720), (1920, 1080), (3840, 2160), (17, 5), (1, 1)])
+@pytest.mark.parametrize("t", [0.0, 1.0, 0.37, 2.5])
+def test_ubershader_bitexact(empty_renderer, w, h, t):
+    img = empty_renderer.render(wl.render_params(w, h, time_sec=t, mode=wl.MODE_UBERSHADER_RT1))
+    ref = pyoracle.ubershader_frame(w, h, t, 0)
+    _cmp(img, ref, f"ubershader {w}x{h} t={t}")
+
+
+def test_debug_view_bitexact(empty_renderer):
+    img = empty_renderer.render(wl.render_params(640, 360, mode=wl.MODE_DEBUG_ST))
+    ref = pyoracle.ubershader_frame(640, 360, 0.0, 1)
+    _cmp(img, ref, "ep_debug_view_1")
+
+
+def test_ubershader_kats_on_gpu(empty_renderer):
+    kats = json.load(open(os.path.join(GOLD, "ubershader_kats.json")))
+    cache = {}
+    for k in kats["pixels"]:
+        key = (k["w"], k["h"], k["t"])
+        if key not in cache:
+            cache[key] = empty_renderer.render(wl.render_params(k["w"], k["h"], time_sec=k["t"]))
+        got = cache[key][k["y"], k["x"], :3]
+        assert np.max(np.abs(got - np.array(k["rgb"]))) < 1e-6, (k, got)
+    img = cache[(256, 256, 0.0)]
+    hits = int(((img[..., 0] < 1.0) & (img[..., 2] < 0.9999999)).sum())
+    assert hits == kats["hit_pixels_256_t0"]
+
+
+def _scene(name, **kw):
+    r = wl.Renderer(name, max_nodes=4096)
+    info = scenes.build(name, r, **kw) if name in scenes.SCENES else None
+    return r, info
+
+
+def _oracle_rows(r, params):
+    prog, nrec, _ = r.program()
+    mats, nm = r.materials()
+    fr = r.frame_desc(params)
+    img, segs = pyoracle.pathtrace_rows(prog, nrec, mats, nm, fr, 0, params.height)
+    return img, segs
+
+
+@pytest.mark.parametrize("scene", ["csg32", "rtiow_cover", "csg256_balanced", "csg256_chain"])
+@pytest.mark.parametrize("mode", [wl.MODE_PATHTRACE, wl.MODE_NORMALS])
+def test_pathtrace_small_frame_bitexact(scene, mode):
+    r, info = _scene(scene)
+    p = info.params(width=96, height=54, spp=8 if mode == wl.MODE_PATHTRACE else 1, mode=mode, seed=7)
+    img = r.render(p)
+    ref, _ = _oracle_rows(r, p)
+    _cmp(img, ref, f"{scene} mode={mode}")
+    r.close()
+
+
+@pytest.mark.parametrize("scene", ["csg32", "rtiow_cover", "csg256_balanced"])
+def test_pathtrace_full_size_sampled_pixels(scene):
+    """BASELINE configs at full size (1920x1080, 64 spp, 8 bounces): the whole frame on
+    the GPU, a random sample of pixels on the oracle."""
+    r, info = _scene(scene)
+    p = info.params()
+    img = r.render(p)
+    assert np.isfinite(img).all()
+    rng = np.random.default_rng(1234)
+    n = 192
+    xs = rng.integers(0, p.width, n).astype(np.uint32)
+    ys = rng.integers(0, p.height, n).astype(np.uint32)
+    prog, nrec, _ = r.program()
+    mats, nm = r.materials()
+    ref, _ = pyoracle.pathtrace_pixels(prog, nrec, mats, nm, r.frame_desc(p), xs, ys)
+    _cmp(img[ys, xs], ref, f"{scene} full-size sampled")
+    r.close()
+
+
+def test_golden_fixtures_on_gpu():
+    man = json.load(open(os.path.join(GOLD, "manifest.json")))
+    for case in man["pathtrace"]:
+        r, info = _scene(case["scene"])
+        p = info.params(width=case["w"], height=case["h"], spp=case["spp"], mode=case["mode"])
+        img = r.render(p)
+        ref = np.fromfile(os.path.join(GOLD, case["file"]), dtype=np.float32).reshape(case["h"], case["w"], 4)
+        _cmp(img, ref, case["name"])
+        r.close()
+
+
+def test_deterministic_and_seed_sensitive():
+    r, info = _scene("csg32")
+    p = info.params(width=128, height=72, spp=4)
+    a = r.render(p)
+    b = r.render(p)
+    assert np.array_equal(a, b)
+    p2 = info.params(width=128, height=72, spp=4, seed=99)
+    c = r.render(p2)
+    assert not np.array_equal(a, c)
+    r.close()
+
+
+def test_sample_offset_splits_average():
+    """spp linearity: mean of two renders over disjoint sample ranges == one render of
+    both ranges (up to fp32 re-association of the per-pixel mean)."""
+    r, info = _scene("csg32")
+    full = r.render(info.params(width=64, height=36, spp=8))
+    h1 = r.render(info.params(width=64, height=36, spp=4, sample_offset=0))
+    h2 = r.render(info.params(width=64, height=36, spp=4, sample_offset=4))
+    np.testing.assert_allclose((h1 + h2) / 2, full, rtol=0, atol=2e-6)
+    r.close()
+
+
+def _torch():
+    import torch
+    return torch
+
+
+@pytest.mark.parametrize("nranks,tile", [(1, 16), (2, 16), (3, 8), (8, 16), (5, 7)])
+def test_row_tiles_assemble_to_full_frame(nranks, tile):
+    torch = _torch()
+    r, info = _scene("csg32")
+    p = info.params(width=200, height=123, spp=2)
+    full = r.render(p)
+    lr = wl.local_rows(p.height, tile, nranks)
+    gathered = torch.zeros((nranks, lr, p.width, 4), dtype=torch.float32, device="cuda")
+    seg = torch.zeros(1, dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for rank in range(nranks):
+        r.render_rows_device(p, gathered[rank].data_ptr(), tile, rank, nranks, stream, seg.data_ptr())
+    frame = torch.empty((p.height, p.width, 4), dtype=torch.float32, device="cuda")
+    wl.assemble_rows_device(gathered.data_ptr(), frame.data_ptr(), p.width, p.height, tile, nranks, stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy(), full)
+    # segment counter == oracle's count for the whole frame
+    _, segs = _oracle_rows(r, p)
+    assert int(seg.item()) == segs
+    r.close()
+
+
+def test_event_window_overflow_restart():
+    """A ray crossing > 8 primitive boundaries exercises the window re-collection path."""
+    r = wl.Renderer("overflow", max_nodes=256)
+    items = []
+    for i in range(24):  # a row of overlapping spheres along -z in front of the camera
+        s = r.sphere(0.6)
+        items.append((s, (0.05 * (i % 3), 0.0, -2.0 - 0.5 * i)))
+    # difference chain makes many events non-flipping
+    node, off = items[0]
+    acc = r.union(wl.arg(node, off), wl.arg(items[1][0], items[1][1]))
+    for k, (s, c) in enumerate(items[2:]):
+        op = r.difference if k % 2 else r.union
+        acc = op(wl.arg(acc), wl.arg(s, c))
+    r.set_camera((0, 0, 0), (0, 0, -1), (0, 1, 0), 30.0)
+    for mode, spp in [(wl.MODE_NORMALS, 1), (wl.MODE_PATHTRACE, 4)]:
+        p = wl.render_params(48, 48, spp=spp, max_depth=6, mode=mode)
+        img = r.render(p)
+        ref, _ = _oracle_rows(r, p)
+        _cmp(img, ref, f"overflow mode={mode}")
+    r.close()
+
+
+def test_edge_scenes():
+    # empty scene: sky only
+    r = wl.Renderer("empty", max_nodes=4)
+    p = wl.render_params(32, 16, spp=2, mode=wl.MODE_PATHTRACE)
+    img = r.render(p)
+    ref, segs = _oracle_rows(r, p)
+    _cmp(img, ref, "empty scene")
+    assert segs == 32 * 16 * 2
+    r.close()
+    # a lone ground half-space (unbounded), a zero-radius sphere, a degenerate normal
+    r = wl.Renderer("edges", max_nodes=16)
+    g = r.halfspace((0, 1, 0))
+    z = r.sphere(0.0)
+    dgn = r.halfspace((0, 0, 0))
+    s = r.sphere(0.5)
+    u = r.union(wl.arg(g, (0, -0.5, 0)), wl.arg(z, (0, 0, -1)))
+    i = r.intersection(wl.arg(dgn), wl.arg(s, (0.3, 0.0, -1.5)))
+    r.union(wl.arg(u), wl.arg(i))
+    r.set_material(s, r.dielectric(1.5))
+    r.set_camera((0, 0.3, 1), (0, 0, -1), (0, 1, 0), 60.0, 0.05, 2.0)
+    for mode, spp in [(wl.MODE_NORMALS, 1), (wl.MODE_PATHTRACE, 4)]:
+        p = wl.render_params(64, 48, spp=spp, max_depth=8, mode=mode)
+        img = r.render(p)
+        ref, _ = _oracle_rows(r, p)
+        _cmp(img, ref, f"edge scene mode={mode}")
+    r.close()
+
+
+def test_draw_frame_demo_path():
+    """The reference's demo flow (main.c:38-51): new, add nodes, isroot, draw."""
+    r = wl.Renderer("Test1Render", max_nodes=8)
+    s1 = r.sphere(1.0)
+    s2 = r.sphere(1.0)
+    b = r.union(wl.arg(s1), wl.arg(s2))
+    assert (r.isroot(s1), r.isroot(s2), r.isroot(b)) == (False, False, True)
+    params = wl.render_params(1280, 720, time_sec=0.0)
+    r.lib.wo_renderer_set_draw_params(r.ptr, ctypes.byref(params), 1)
+    r.lib.wo_renderer_draw_frame(r.ptr)
+    assert wl.last_error() == "" or "draw" not in wl.last_error()
+    r.close()
