@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--tile-rows", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-json", default=None,
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-dispatch HBM bytes measured by rocprofv3 --pmc (profiles/*.json) for roofline.traffic")
     return ap.parse_args()
 
@@ -199,19 +199,21 @@ def cpu_baseline(r, params, budget_s: float):
     prog, nrec, _ = r.program()
     mats, nm = r.materials()
     fr = r.frame_desc(params)
-    row = params.height // 2
+    # whole rows starting at the middle of the frame, wrapping, until the budget is spent
+    start = params.height // 2
+    row = start
     rows = 0
     segs = 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s and row < params.height:
-        n = min(nthreads // 4 + 1, params.height - row)
+    while time.perf_counter() - t0 < budget_s and rows < params.height:
+        n = min(nthreads // 4 + 1, params.height - row, params.height - rows)
         _, s = pyoracle.pathtrace_rows(prog, nrec, mats, nm, fr, row, n, nthreads=nthreads)
         segs += s
         rows += n
-        row += n
+        row = (row + n) % params.height
     dt = time.perf_counter() - t0
     return {"value": round(segs / dt / 1e6, 4), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
-            "sample": f"rows {params.height // 2}..{params.height // 2 + rows - 1} ({rows} of {params.height}) of the "
+            "sample": f"{rows} of {params.height} rows (from row {start}, wrapping) of the "
                       f"same {params.width}x{params.height} frame, {params.spp} spp, {params.max_depth} bounces; "
                       f"{segs} segments in {dt:.1f} s"}
 

@@ -550,6 +550,14 @@ int wo_compile_scene(Wo_Renderer* r, char* err, size_t errlen) {
         free(c.prog);
         return -1;
     }
+    if (!c.prog) { /* empty scene: keep a valid (zero-record) program pointer */
+        c.prog = (WoRec*)calloc(1, sizeof(WoRec));
+        c.cap_recs = 1;
+        if (!c.prog) {
+            snprintf(err, errlen, "out of host memory");
+            return -1;
+        }
+    }
     free(r->prog);
     r->prog = c.prog;
     r->n_recs = c.n_recs;
