@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--tile-rows", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--jit", type=int, default=1, help="1: scene-specialised kernel (auto), 0: interpreter kernel")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-dispatch HBM bytes measured by rocprofv3 --pmc (profiles/*.json) for roofline.traffic")
     return ap.parse_args()
@@ -81,6 +82,7 @@ def main():
     if args.spp:
         over["spp"] = args.spp
     params = info.params(**over)
+    r.set_jit(args.jit)
     W, H, T = params.width, params.height, args.tile_rows
     lr = wl.local_rows(H, T, world)
     out = torch.empty((lr, W, 4), dtype=torch.float32, device=dev)
@@ -144,7 +146,7 @@ def main():
                     "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4), "traffic": None,
                     "kernel": "pathtrace_kernel", "kernel_ms": round(k_ms, 4),
                     "flop_per_segment": info.flop_per_segment,
-                    "segments_per_launch": segs_local // steps}
+                    "segments_per_launch": segs_local // steps, "trace_path": r.trace_path()}
         else:
             value = W * H * steps / elapsed_s / 1e6
             bytes_launch = lr * W * 16

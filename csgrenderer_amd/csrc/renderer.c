@@ -100,6 +100,10 @@ Wo_Renderer* wo_renderer_new(Wo_App* app, char const* name, size_t max_node_coun
     }
     r->t0 = wo_monotonic_sec();
     r->dirty = 1;
+    {
+        const char* j = getenv("WOLOLO_JIT");
+        r->jit_mode = (j && strcmp(j, "0") == 0) ? 0 : 1;
+    }
     r->device = -1;
 
     char err[256] = {0};
@@ -348,8 +352,43 @@ static int sync_device(Wo_Renderer* r) {
             return -1;
         }
         r->dev_stale = 0;
+        r->jit_loaded = 0;
+        uint32_t max_prims = 256;
+        const char* mp = getenv("WOLOLO_JIT_MAX_PRIMS");
+        if (mp && *mp) max_prims = (uint32_t)strtoul(mp, NULL, 10);
+        if (r->jit_mode && r->n_prims > 0 && r->n_prims <= max_prims) {
+            char* src = wo_generate_jit_source(r->prog, r->n_recs, r->n_prims);
+            if (!src) {
+                fprintf(stderr, WO_LOG_PREFIX " scene specialisation: source generation failed; using the interpreter\n");
+            } else if (wo_dev_set_jit(r->dev, src, err, sizeof err) != 0) {
+                fprintf(stderr, WO_LOG_PREFIX " scene specialisation failed (%s); using the interpreter kernel\n", err);
+            } else {
+                r->jit_loaded = 1;
+            }
+            free(src);
+        }
+        if (!r->jit_loaded) (void)wo_dev_set_jit(r->dev, NULL, err, sizeof err);
     }
     return 0;
+}
+
+void wo_renderer_set_jit(Wo_Renderer* r, int mode) {
+    if (r->jit_mode != (mode ? 1 : 0)) {
+        r->jit_mode = mode ? 1 : 0;
+        r->dev_stale = 1;
+    }
+}
+
+char* wo_renderer_jit_source(Wo_Renderer* r) {
+    if (wo_renderer_compile(r) < 0 || r->n_prims == 0) return NULL;
+    return wo_generate_jit_source(r->prog, r->n_recs, r->n_prims);
+}
+
+void wo_free(void* p) { free(p); }
+
+char const* wo_renderer_trace_path(Wo_Renderer* r) {
+    if (!r->dev) return "none";
+    return r->jit_loaded ? "jit" : "interpreter";
 }
 
 int wo_renderer_render_f32(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba) {

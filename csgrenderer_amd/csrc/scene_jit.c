@@ -1,0 +1,272 @@
+/*
+ * scene_jit.c -- generates a scene-specialised HIP trace kernel from the
+ * compiled CSG program (wo_scene.h).  The source is compiled at scene upload by
+ * hiprtc (trace_kernels.hip: wo_dev_upload_scene), the way a Vulkan renderer
+ * builds a pipeline for its shaders (ref renderer.c:1135-1280 loads the SPIR-V
+ * and builds the pipeline at init).
+ *
+ * What specialisation buys over the interpreter kernel:
+ *   - leaf parameters become fp32 literals (no LDS/global reads, no VGPRs);
+ *   - BOUND culling becomes a scalar branch around the subtree's code, its
+ *     ballot result kept in an SGPR for the later evaluations;
+ *   - the CSG evaluation becomes straight-line bit operations on named values
+ *     (1 VALU per node) instead of a decoded postfix walk.
+ * The arithmetic, event order and tie-breaking are exactly the interpreter's
+ * (wo_device_common.h), so both paths agree bit-for-bit with the oracle.
+ */
+#include <inttypes.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "wo_internal.h"
+
+typedef struct Buf {
+    char* s;
+    size_t n, cap;
+    int oom;
+} Buf;
+
+static void bput(Buf* b, const char* fmt, ...) {
+    if (b->oom) return;
+    for (;;) {
+        va_list ap;
+        va_start(ap, fmt);
+        size_t room = b->cap - b->n;
+        int k = vsnprintf(b->s ? b->s + b->n : NULL, b->s ? room : 0, fmt, ap);
+        va_end(ap);
+        if (k < 0) {
+            b->oom = 1;
+            return;
+        }
+        if (b->s && (size_t)k < room) {
+            b->n += (size_t)k;
+            return;
+        }
+        size_t nc = b->cap ? b->cap * 2 : 1 << 16;
+        while (nc < b->n + (size_t)k + 1) nc *= 2;
+        char* ns = (char*)realloc(b->s, nc);
+        if (!ns) {
+            b->oom = 1;
+            return;
+        }
+        b->s = ns;
+        b->cap = nc;
+    }
+}
+
+/* fp32 literal that round-trips exactly */
+static void flit(char out[48], float v) {
+    if (v != v) {
+        snprintf(out, 48, "__builtin_nanf(\"\")");
+    } else if (v == __builtin_inff()) {
+        snprintf(out, 48, "wodev::kInf");
+    } else if (v == -__builtin_inff()) {
+        snprintf(out, 48, "(-wodev::kInf)");
+    } else {
+        snprintf(out, 48, "%af", (double)v);
+    }
+}
+
+typedef struct Gen {
+    const WoRec* prog;
+    uint32_t n;
+    Buf* b;
+    uint32_t nbound;  /* BOUND counter (cull flag names) */
+    uint32_t nval;    /* value counter (eval temporaries) */
+    int err;
+} Gen;
+
+/* ---- collect: intersect every primitive of [start, end), fill the window ---- */
+static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
+    uint32_t pc = start;
+    while (pc < end && !g->err) {
+        const WoRec* r = &g->prog[pc];
+        if (r->op == WO_OP_BOUND) {
+            char c0[48], c1[48], c2[48], c3[48], c4[48];
+            flit(c0, r->f[0]);
+            flit(c1, r->f[1]);
+            flit(c2, r->f[2]);
+            flit(c3, r->f[3]);
+            flit(c4, r->f[4]);
+            uint32_t k = g->nbound++;
+            bput(g->b, "%*sif (first) c%u = __ballot(wodev::bound_may_hit(%s, %s, %s, %s, %s, o, d)) != 0ull;\n",
+                 indent, "", k, c0, c1, c2, c3, c4);
+            bput(g->b, "%*sif (c%u) {\n", indent, "", k);
+            gen_collect(g, pc + 1, r->u0, indent + 2);
+            bput(g->b, "%*s}\n", indent, "");
+            pc = r->u0;
+        } else if (r->op == WO_OP_PRIM) {
+            uint32_t ord = r->u1, cnt = r->u0;
+            bput(g->b, "%*s{  // primitive %u (%u leaves)\n", indent, "", ord, cnt);
+            bput(g->b, "%*s  wodev::Ivl iv; wodev::ivl_init(iv); float la, lb;\n", indent, "");
+            for (uint32_t m = 0; m < cnt; ++m) {
+                const WoRec* L = &g->prog[pc + 1 + m];
+                char a[48], b[48], c[48], e[48];
+                flit(a, L->f[0]);
+                flit(b, L->f[1]);
+                flit(c, L->f[2]);
+                flit(e, L->f[3]);
+                bput(g->b, "%*s  wodev::%s_interval(%s, %s, %s, %s, o, d, la, lb); wodev::ivl_meet(iv, la, lb, %uu);\n",
+                     indent, "", L->op == WO_LEAF_SPHERE ? "sphere" : "halfspace", a, b, c, e, m);
+            }
+            bput(g->b,
+                 "%*s  if (!(iv.a > iv.b)) {\n"
+                 "%*s    if (first) bits[%u] |= ((iv.a <= tmin && iv.b > tmin) ? 1u : 0u) << %u;\n"
+                 "%*s    if (iv.a > tmin) { uint64_t k = wodev::event_key(iv.a, %uu, 0u, iv.ma); if (k > after) "
+                 "win.insert(k); }\n"
+                 "%*s    if (iv.b > tmin && iv.b < wodev::kInf) { uint64_t k = wodev::event_key(iv.b, %uu, 1u, iv.mb); "
+                 "if (k > after) win.insert(k); }\n"
+                 "%*s  }\n%*s}\n",
+                 indent, "", indent, "", ord / 32, ord % 32, indent, "", ord, indent, "", ord, indent, "", indent,
+                 "");
+            pc += 1 + cnt;
+        } else {
+            ++pc; /* binops: nothing to collect */
+        }
+    }
+}
+
+/* ---- eval: value of the subtree [start, end) as named 0/1 temporaries ---- */
+static uint32_t gen_eval(Gen* g, uint32_t start, uint32_t end, int indent) {
+    uint32_t stack[64];
+    int sp = 0;
+    uint32_t pc = start;
+    while (pc < end && !g->err) {
+        const WoRec* r = &g->prog[pc];
+        if (r->op == WO_OP_BOUND) {
+            uint32_t k = g->nbound++;
+            uint32_t v = g->nval++;
+            bput(g->b, "%*suint32_t v%u;\n%*sif (c%u) {\n", indent, "", v, indent, "", k);
+            uint32_t inner = gen_eval(g, pc + 1, r->u0, indent + 2);
+            bput(g->b, "%*s  v%u = v%u;\n%*s} else {\n%*s  v%u = 0u;\n%*s}\n", indent, "", v, inner, indent, "",
+                 indent, "", v, indent, "");
+            if (sp >= 64) {
+                g->err = 1;
+                return 0;
+            }
+            stack[sp++] = v;
+            pc = r->u0;
+        } else if (r->op == WO_OP_PRIM) {
+            uint32_t v = g->nval++;
+            bput(g->b, "%*suint32_t v%u = (bits[%u] >> %u) & 1u;\n", indent, "", v, r->u1 / 32, r->u1 % 32);
+            if (sp >= 64) {
+                g->err = 1;
+                return 0;
+            }
+            stack[sp++] = v;
+            pc += 1 + r->u0;
+        } else {
+            if (sp < 2) {
+                g->err = 1;
+                return 0;
+            }
+            uint32_t B = stack[--sp], A = stack[--sp];
+            uint32_t v = g->nval++;
+            const char* fmt = r->op == WO_OP_UNION   ? "%*suint32_t v%u = v%u | v%u;\n"
+                              : r->op == WO_OP_INTER ? "%*suint32_t v%u = v%u & v%u;\n"
+                              : r->op == WO_OP_DIFF  ? "%*suint32_t v%u = v%u & (v%u ^ 1u);\n"
+                                                     : NULL;
+            if (fmt)
+                bput(g->b, fmt, indent, "", v, A, B);
+            else /* RDIFF: B & ~A */
+                bput(g->b, "%*suint32_t v%u = v%u & (v%u ^ 1u);\n", indent, "", v, B, A);
+            stack[sp++] = v;
+            ++pc;
+        }
+    }
+    if (sp != 1) {
+        g->err = 1;
+        return 0;
+    }
+    return stack[0];
+}
+
+char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prims) {
+    Buf b = {0};
+    Gen g;
+    memset(&g, 0, sizeof g);
+    g.prog = prog;
+    g.n = n_recs;
+    g.b = &b;
+    uint32_t nw = n_prims ? (n_prims + 31u) / 32u : 1u;
+    uint32_t nbounds = 0;
+    for (uint32_t i = 0; i < n_recs; ++i) nbounds += prog[i].op == WO_OP_BOUND;
+
+    bput(&b, "// generated by scene_jit.c: %u records, %u primitives, %u bounds\n", n_recs, n_prims, nbounds);
+    bput(&b, "#include \"wo_device_common.h\"\n\n");
+    bput(&b, "__constant__ uint32_t kOrdPc[%u] = {", n_prims ? n_prims : 1u);
+    if (!n_prims) bput(&b, "0u");
+    for (uint32_t i = 0, o = 0; i < n_recs; ++i)
+        if (prog[i].op == WO_OP_PRIM) bput(&b, "%s%uu", o++ ? ", " : "", i);
+    bput(&b, "};\n\n");
+    bput(&b,
+         "struct JitTracer {\n"
+         "  const WoRec* __restrict__ prog;\n"
+         "  __device__ __forceinline__ WoRec hit_leaf(const wodev::Hit& h) const {\n"
+         "    return prog[kOrdPc[h.ord] + 1u + h.member];\n"
+         "  }\n"
+         "  __device__ __forceinline__ bool trace(wodev::F3 o, wodev::F3 d, wodev::Hit& hit) {\n");
+    if (n_prims == 0) {
+        bput(&b, "    return false;\n  }\n};\n");
+    } else {
+        bput(&b, "    const float tmin = WO_T_MIN;\n");
+        bput(&b, "    uint32_t bits[%u];\n", nw);
+        for (uint32_t w = 0; w < nw; ++w) bput(&b, "    bits[%u] = 0u;\n", w);
+        for (uint32_t k = 0; k < nbounds; ++k) bput(&b, "    bool c%u = true;\n", k);
+        bput(&b,
+             "    wodev::Window win; win.clear();\n"
+             "    bool collect = true, first = true, have = false;\n"
+             "    uint64_t after = 0ull, key = 0ull;\n"
+             "    uint32_t root = 0u;\n"
+             "    for (;;) {\n"
+             "      if (collect) {\n");
+        g.nbound = 0;
+        gen_collect(&g, 0, n_recs, 8);
+        bput(&b,
+             "        collect = false;\n"
+             "        if (first && win.k[0] == wodev::kEmptyKey) return false;\n"
+             "        first = false;\n"
+             "      }\n"
+             "      uint32_t r;\n"
+             "      {\n");
+        g.nbound = 0;
+        uint32_t rv = gen_eval(&g, 0, n_recs, 8);
+        bput(&b, "        r = v%u;\n      }\n", rv);
+        bput(&b,
+             "      if (have && r != root) { wodev::hit_from_key(key, r, hit); return true; }\n"
+             "      root = r;\n"
+             "      if (win.k[0] == wodev::kEmptyKey) {\n"
+             "        if (!win.dropped) return false;\n"
+             "        after = key; win.clear(); collect = true; have = false;\n"
+             "        continue;\n"
+             "      }\n"
+             "      key = win.pop();\n"
+             "      have = true;\n"
+             "      {\n"
+             "        uint32_t ord = ((uint32_t)key) >> 12;\n"
+             "        uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n");
+        for (uint32_t w = 0; w < nw; ++w) bput(&b, "        bits[%u] ^= w == %uu ? m : 0u;\n", w, w);
+        bput(&b,
+             "      }\n"
+             "    }\n"
+             "  }\n"
+             "};\n");
+    }
+    bput(&b,
+         "\nextern \"C\" __global__ __launch_bounds__(256) void wo_jit_pathtrace(\n"
+         "    const WoRec* __restrict__ prog, const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t local_rows,\n"
+         "    float4* __restrict__ out, unsigned long long* __restrict__ seg_out) {\n"
+         "  JitTracer tr;\n"
+         "  tr.prog = prog;\n"
+         "  uint32_t lx, lrow;\n"
+         "  wodev::block_pixel(threadIdx.x, lx, lrow);\n"
+         "  wodev::pathtrace_pixel(tr, mats, fr, lx, lrow, local_rows, out, seg_out, threadIdx.x & 63u);\n"
+         "}\n");
+    if (g.err || b.oom) {
+        free(b.s);
+        return NULL;
+    }
+    return b.s;
+}

@@ -1,214 +1,47 @@
-// trace_kernels.hip -- the per-pixel hot path of the wololo renderer, written for
-// gfx950 (MI355X, CDNA4, wave64).  Replaces the reference's fragment stage:
-//   src/wololo/renderer/ubershader1.frag:19-163 (ray generation, hit_sphere,
-//   ray_color, ep_rt1_1 / ep_debug_view_1), launched by the reference as one
-//   fragment invocation per pixel from draw_frame_with_renderer
-//   (renderer.c:2085-2219).
+// trace_kernels.hip -- the per-pixel hot path of the wololo renderer for gfx950
+// (MI355X, CDNA4, wave64).  Replaces the reference's fragment stage
+// (src/wololo/renderer/ubershader1.frag:19-163, one invocation per pixel,
+// launched by draw_frame_with_renderer, renderer.c:2085-2219).
 //
 // Kernels
-//   ubershader_kernel  -- the reference shader, restated bit-for-bit in IEEE fp32
-//                         (sin hoisted to the host).  HBM-store bound: 16 B/pixel.
-//   pathtrace_kernel   -- north-star path: CSG program evaluation (stackless,
-//                         bit-stack over a postfix program), spheres + half-spaces,
-//                         lambertian / metal / dielectric, spp x bounces with
-//                         path regeneration.  FP32-VALU bound.
-//   assemble_kernel    -- un-interleaves row-cyclic rank tiles after the gather.
-//
-// Numerics: the whole file is compiled with contraction off, and hipcc lowers
-// fp32 '/' and sqrtf to correctly rounded sequences on gfx950
-// (v_div_scale/fmas/fixup, v_sqrt + ulp fix-up), so every result is reproducible
-// bit-for-bit by the C oracle (oracle/oracle.c) compiled with -ffp-contract=off.
+//   ubershader_kernel  the reference shader restated bit-for-bit in IEEE fp32
+//                      (sin hoisted to the host).  HBM-store bound, 16 B/pixel.
+//   pathtrace_kernel   CSG path tracer, INTERPRETER form: walks the compiled
+//                      postfix program (staged in LDS when it fits), wave-uniform
+//                      BOUND culling, sorted event window, bit-stack evaluation.
+//   wo_jit_pathtrace   the same path tracer SPECIALISED per scene: source from
+//                      scene_jit.c, compiled here with hiprtc at scene upload.
+//   assemble_kernel    un-interleaves row-cyclic rank tiles after the gather.
+// The shared device code (math, RNG, leaves, event window, shading, path loop)
+// is wo_device_common.h; both forms agree bit-for-bit with oracle/oracle.c.
 #include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
 
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
 #include "wo_dev.h"
+#include "wo_device_common.h"
 #include "wololo/wo_scene.h"
+
+#include "jit_sources.inc"
 
 #pragma clang fp contract(off)
 
 namespace {
 
-constexpr uint32_t kBlock = 256;       // 4 waves
-constexpr uint32_t kPtTile = 16;       // pathtrace block = 16x16 pixels, waves = 8x8
-constexpr int kWindow = 8;             // sorted event window per lane (registers)
-constexpr uint32_t kEmptyKey32 = 0xFFFFFFFFu;
-constexpr uint64_t kEmptyKey = ~0ull;
-constexpr float kInf = __builtin_inff();
+using namespace wodev;
 
 // 4-bit op codes of the per-wave compacted program (8 per dword).
-constexpr uint32_t kCodePrim = 1, kCodeUnion = 2, kCodeInter = 3, kCodeDiff = 4, kCodeRdiff = 5,
-                   kCodeConst0 = 6;
-
-struct F3 {
-    float x, y, z;
-};
-
-__device__ __forceinline__ F3 f3(float x, float y, float z) {
-    F3 r;
-    r.x = x;
-    r.y = y;
-    r.z = z;
-    return r;
-}
-__device__ __forceinline__ float dot3(F3 a, F3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
-__device__ __forceinline__ F3 unit3(F3 v) {
-    float inv = 1.0f / sqrtf(dot3(v, v));
-    return f3(v.x * inv, v.y * inv, v.z * inv);
-}
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-
-// ---------------------------------------------------------------------------
-// Counter-based RNG (PCG-RXS-M-XS 32), identical to oracle.c.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t pcg_hash(uint32_t v) {
-    uint32_t s = v * 747796405u + 2891336453u;
-    uint32_t w = ((s >> ((s >> 28u) + 4u)) ^ s) * 277803737u;
-    return (w >> 22u) ^ w;
-}
-struct Rng {
-    uint32_t s;
-    __device__ __forceinline__ uint32_t next() {
-        s = s * 747796405u + 2891336453u;
-        uint32_t w = ((s >> ((s >> 28u) + 4u)) ^ s) * 277803737u;
-        return (w >> 22u) ^ w;
-    }
-    __device__ __forceinline__ float uniform() { return (float)(next() >> 8) * 0x1p-24f; }
-};
-
-__device__ __forceinline__ F3 random_in_unit_sphere(Rng& rng) {
-    for (int i = 0; i < 64; ++i) {
-        float x = 2.0f * rng.uniform() - 1.0f;
-        float y = 2.0f * rng.uniform() - 1.0f;
-        float z = 2.0f * rng.uniform() - 1.0f;
-        F3 p = f3(x, y, z);
-        float l2 = dot3(p, p);
-        if (l2 < 1.0f && l2 > 1e-12f) return p;
-    }
-    return f3(0.0f, 0.0f, 1.0f);
-}
-
-// ---------------------------------------------------------------------------
-// Leaf intersections.  Intervals [a, b]; empty = (+inf, -inf).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void leaf_interval(const WoRec& L, uint32_t kind, F3 o, F3 d, float& la, float& lb) {
-    if (kind == WO_LEAF_SPHERE) {
-        float fx = o.x - L.f[0], fy = o.y - L.f[1], fz = o.z - L.f[2];
-        float b = (fx * d.x + fy * d.y) + fz * d.z;
-        float lx = fx - b * d.x, ly = fy - b * d.y, lz = fz - b * d.z;
-        float ll = (lx * lx + ly * ly) + lz * lz;
-        float disc = L.f[3] - ll;
-        if (disc < 0.0f) {
-            la = kInf;
-            lb = -kInf;
-        } else {
-            float s = sqrtf(disc);
-            float nb = -b;
-            la = nb - s;
-            lb = nb + s;
-        }
-    } else {
-        float den = (L.f[0] * d.x + L.f[1] * d.y) + L.f[2] * d.z;
-        float no = (L.f[0] * o.x + L.f[1] * o.y) + L.f[2] * o.z;
-        float dist = L.f[3] - no;
-        if (den == 0.0f) {
-            if (dist >= 0.0f) {
-                la = -kInf;
-                lb = kInf;
-            } else {
-                la = kInf;
-                lb = -kInf;
-            }
-        } else {
-            float t = dist / den;
-            if (den > 0.0f) {
-                la = -kInf;
-                lb = t;
-            } else {
-                la = t;
-                lb = kInf;
-            }
-        }
-    }
-}
-
-struct Ivl {
-    float a, b;
-    uint32_t ma, mb;
-};
-
-// Convex primitive = intersection of its member leaves.  Ties keep the first member.
-template <class Prog>
-__device__ __forceinline__ Ivl prim_interval(Prog prog, uint32_t pc, uint32_t count, F3 o, F3 d) {
-    Ivl iv;
-    iv.a = -kInf;
-    iv.b = kInf;
-    iv.ma = 0;
-    iv.mb = 0;
-    for (uint32_t m = 0; m < count; ++m) {
-        WoRec L = prog[pc + 1u + m];
-        uint32_t kind = uni(L.op);
-        float la, lb;
-        leaf_interval(L, kind, o, d, la, lb);
-        if (la > iv.a) {
-            iv.a = la;
-            iv.ma = m;
-        }
-        if (lb < iv.b) {
-            iv.b = lb;
-            iv.mb = m;
-        }
-    }
-    return iv;
-}
-
-// Conservative "may the ray [0, inf) touch this bounding sphere" test.  The
-// 4e-6*tca^2 slack covers fp32 rounding of the perpendicular distance.
-__device__ __forceinline__ bool bound_may_hit(const WoRec& B, F3 o, F3 d) {
-    float ox = B.f[0] - o.x, oy = B.f[1] - o.y, oz = B.f[2] - o.z;
-    float tca = (ox * d.x + oy * d.y) + oz * d.z;
-    float lx = ox - tca * d.x, ly = oy - tca * d.y, lz = oz - tca * d.z;
-    float d2 = (lx * lx + ly * ly) + lz * lz;
-    bool miss = (d2 > B.f[3] + 4e-6f * (tca * tca)) || (tca + B.f[4] < 0.0f);
-    return !miss;
-}
-
-// Event key: (t, primitive ordinal, type) lexicographic == one u64 compare,
-// because t > WO_T_MIN > 0 makes the float bits monotone.  The low 11 bits
-// carry the member leaf that produced the event (for the normal).
-__device__ __forceinline__ uint64_t event_key(float t, uint32_t ord, uint32_t type, uint32_t member) {
-    return ((uint64_t)__float_as_uint(t) << 32) | (uint64_t)((ord << 12) | (type << 11) | member);
-}
-
-// Sorted insertion into the register window (drops the largest on overflow).
-struct Window {
-    uint64_t k[kWindow];
-    bool dropped;
-    __device__ __forceinline__ void clear() {
-#pragma unroll
-        for (int i = 0; i < kWindow; ++i) k[i] = kEmptyKey;
-        dropped = false;
-    }
-    __device__ __forceinline__ void insert(uint64_t key) {
-        dropped |= (k[kWindow - 1] != kEmptyKey);
-#pragma unroll
-        for (int i = kWindow - 1; i > 0; --i) {
-            uint64_t prev = k[i - 1];
-            uint64_t cur = k[i];
-            k[i] = key < prev ? prev : (key < cur ? key : cur);
-        }
-        k[0] = key < k[0] ? key : k[0];
-    }
-    __device__ __forceinline__ uint64_t pop() {
-        uint64_t r = k[0];
-#pragma unroll
-        for (int i = 0; i < kWindow - 1; ++i) k[i] = k[i + 1];
-        k[kWindow - 1] = kEmptyKey;
-        return r;
-    }
-};
+constexpr uint32_t kCodePrim = 1, kCodeUnion = 2, kCodeInter = 3, kCodeDiff = 4, kCodeConst0 = 6;
 
 // Per-wave LDS scratch layout (dwords), computed on the host.
 struct KLayout {
@@ -218,7 +51,29 @@ struct KLayout {
     uint32_t wave_words;   // stride between waves
 };
 
-struct Trace {
+struct ProgPtr {
+    const WoRec* p;
+    __device__ __forceinline__ WoRec operator[](uint32_t i) const { return p[i]; }
+};
+
+template <class Prog>
+__device__ __forceinline__ Ivl prim_interval(Prog prog, uint32_t pc, uint32_t count, F3 o, F3 d) {
+    Ivl iv;
+    ivl_init(iv);
+    for (uint32_t m = 0; m < count; ++m) {
+        WoRec L = prog[pc + 1u + m];
+        uint32_t kind = uni(L.op);
+        float la, lb;
+        leaf_interval(L, kind, o, d, la, lb);
+        ivl_meet(iv, la, lb, m);
+    }
+    return iv;
+}
+
+// Interpreter: walks the program record by record (wave-uniform pc).
+struct InterpTracer {
+    ProgPtr prog;
+    uint32_t nrec;
     uint32_t* codes;
     uint32_t* ordpc;
     uint32_t* hib;
@@ -240,7 +95,7 @@ struct Trace {
             hib[w * 64u + lane] ^= 1u << ((ord - 64u) & 31u);
         }
     }
-    // Evaluate the root over the compacted program with a 32-deep bit stack.
+    // Root value over the compacted program, 32-deep bit stack.
     __device__ __forceinline__ uint32_t eval_root() const {
         uint32_t st = 0, ord = 0;
         uint32_t nwords = (ncodes + 7u) >> 3;
@@ -271,116 +126,99 @@ struct Trace {
         }
         return st & 1u;
     }
-};
 
-struct Hit {
-    float t;
-    uint32_t ord, type, member;
-    uint32_t root_after;  // 1: the ray enters the solid here
-};
+    __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const { return prog[ordpc[h.ord] + 1u + h.member]; }
 
-// Nearest boundary crossing of the CSG root after WO_T_MIN along o + t d
-// (|d| = 1).  Must be called by every lane that wants a result; lanes that are
-// not tracing must be masked off by the caller.
-template <class Prog>
-__device__ __forceinline__ bool trace(Prog prog, uint32_t nrec, Trace& tr, F3 o, F3 d, Hit& hit) {
-    const float tmin = WO_T_MIN;
-    Window win;
-    win.clear();
-    tr.bits = 0;
-    tr.ncodes = 0;
-    tr.nprims = 0;
-    uint32_t code_acc = 0;
-    uint32_t hib_acc = 0;
+    // Nearest change of the root's membership after WO_T_MIN along o + t d.
+    __device__ __forceinline__ bool trace(F3 o, F3 d, Hit& hit) {
+        const float tmin = WO_T_MIN;
+        Window win;
+        win.clear();
+        bits = 0;
+        ncodes = 0;
+        nprims = 0;
+        uint32_t code_acc = 0;
+        uint32_t hib_acc = 0;
 
-    // ---- pass 1: walk the program (wave-uniform pc), cull, intersect, collect.
-    uint32_t pc = 0;
-    while (pc < nrec) {
-        WoRec rec = prog[pc];
-        uint32_t op = uni(rec.op);
-        uint32_t code;
-        if (op == WO_OP_BOUND) {
-            bool may = bound_may_hit(rec, o, d);
-            if (__ballot(may) != 0ull) {
-                ++pc;
-                continue;
-            }
-            code = kCodeConst0;
-            pc = uni(rec.u0);
-        } else if (op == WO_OP_PRIM) {
-            uint32_t count = uni(rec.u0);
-            uint32_t ord = tr.nprims;
-            Ivl iv = prim_interval(prog, pc, count, o, d);
-            uint32_t inside = 0;
-            if (!(iv.a > iv.b)) {
-                inside = (iv.a <= tmin && iv.b > tmin) ? 1u : 0u;
-                if (iv.a > tmin) win.insert(event_key(iv.a, ord, 0u, iv.ma));
-                if (iv.b > tmin && iv.b < kInf) win.insert(event_key(iv.b, ord, 1u, iv.mb));
-            }
-            if (ord < 64u) {
-                tr.bits |= (uint64_t)inside << ord;
-            } else {
-                uint32_t sh = (ord - 64u) & 31u;
-                hib_acc |= inside << sh;
-                if (sh == 31u) {
-                    tr.hib[((ord - 64u) >> 5) * 64u + tr.lane] = hib_acc;
-                    hib_acc = 0;
+        // pass 1: walk the program, cull, intersect, collect events
+        uint32_t pc = 0;
+        while (pc < nrec) {
+            WoRec rec = prog[pc];
+            uint32_t op = uni(rec.op);
+            uint32_t code;
+            if (op == WO_OP_BOUND) {
+                bool may = bound_may_hit(rec.f[0], rec.f[1], rec.f[2], rec.f[3], rec.f[4], o, d);
+                if (__ballot(may) != 0ull) {
+                    ++pc;
+                    continue;
                 }
+                code = kCodeConst0;
+                pc = uni(rec.u0);
+            } else if (op == WO_OP_PRIM) {
+                uint32_t count = uni(rec.u0);
+                uint32_t ord = nprims;
+                Ivl iv = prim_interval(prog, pc, count, o, d);
+                uint32_t inside = 0;
+                if (!(iv.a > iv.b)) {
+                    inside = (iv.a <= tmin && iv.b > tmin) ? 1u : 0u;
+                    if (iv.a > tmin) win.insert(event_key(iv.a, ord, 0u, iv.ma));
+                    if (iv.b > tmin && iv.b < kInf) win.insert(event_key(iv.b, ord, 1u, iv.mb));
+                }
+                if (ord < 64u) {
+                    bits |= (uint64_t)inside << ord;
+                } else {
+                    uint32_t sh = (ord - 64u) & 31u;
+                    hib_acc |= inside << sh;
+                    if (sh == 31u) {
+                        hib[((ord - 64u) >> 5) * 64u + lane] = hib_acc;
+                        hib_acc = 0;
+                    }
+                }
+                ordpc[ord] = pc;
+                nprims = ord + 1u;
+                code = kCodePrim;
+                pc += 1u + count;
+            } else {
+                code = op;  // WO_OP_UNION..RDIFF share values with the codes
+                ++pc;
             }
-            tr.ordpc[ord] = pc;
-            tr.nprims = ord + 1u;
-            code = kCodePrim;
-            pc += 1u + count;
-        } else {
-            code = op;  // WO_OP_UNION..RDIFF share values with the codes
-            ++pc;
+            uint32_t slot = ncodes & 7u;
+            code_acc |= code << (4u * slot);
+            if (slot == 7u) {
+                codes[ncodes >> 3] = code_acc;
+                code_acc = 0;
+            }
+            ++ncodes;
         }
-        uint32_t slot = tr.ncodes & 7u;
-        code_acc |= code << (4u * slot);
-        if (slot == 7u) {
-            tr.codes[tr.ncodes >> 3] = code_acc;
-            code_acc = 0;
-        }
-        ++tr.ncodes;
-    }
-    if (tr.ncodes & 7u) tr.codes[tr.ncodes >> 3] = code_acc;
-    if (tr.nprims > 64u && ((tr.nprims - 64u) & 31u)) tr.hib[((tr.nprims - 64u) >> 5) * 64u + tr.lane] = hib_acc;
+        if (ncodes & 7u) codes[ncodes >> 3] = code_acc;
+        if (nprims > 64u && ((nprims - 64u) & 31u)) hib[((nprims - 64u) >> 5) * 64u + lane] = hib_acc;
 
-    // ---- pass 2: sweep events in key order; first root flip is the hit.
-    bool found = false;
-    if (win.k[0] == kEmptyKey) return false;
-    uint32_t root = tr.eval_root();
-    for (;;) {
+        // pass 2: sweep events in key order; the first root flip is the hit
+        if (win.k[0] == kEmptyKey) return false;
+        uint32_t root = eval_root();
         while (win.k[0] != kEmptyKey) {
             uint64_t key = win.pop();
-            uint32_t lo = (uint32_t)key;
-            uint32_t ord = lo >> 12;
-            tr.toggle(ord);
-            uint32_t r = tr.eval_root();
+            uint32_t ord = ((uint32_t)key) >> 12;
+            toggle(ord);
+            uint32_t r = eval_root();
             if (r != root) {
-                hit.t = __uint_as_float((uint32_t)(key >> 32));
-                hit.ord = ord;
-                hit.type = (lo >> 11) & 1u;
-                hit.member = lo & 2047u;
-                hit.root_after = r;
-                found = true;
-                win.dropped = false;
-                break;
+                hit_from_key(key, r, hit);
+                return true;
             }
             root = r;
             if (win.k[0] == kEmptyKey && win.dropped) {
-                // Window exhausted but events were dropped: re-collect the
-                // events strictly after `key` (membership state carries on).
+                // window exhausted but events were dropped: re-collect the events
+                // strictly after `key` (the membership state carries on)
                 win.clear();
                 uint32_t ordc = 0;
-                uint32_t nwords = (tr.ncodes + 7u) >> 3;
+                uint32_t nwords = (ncodes + 7u) >> 3;
                 for (uint32_t w = 0; w < nwords; ++w) {
-                    uint32_t word = uni(tr.codes[w]);
-                    uint32_t n = tr.ncodes - w * 8u;
+                    uint32_t word = uni(codes[w]);
+                    uint32_t n = ncodes - w * 8u;
                     n = n < 8u ? n : 8u;
                     for (uint32_t j = 0; j < n; ++j) {
                         if (((word >> (4u * j)) & 15u) != kCodePrim) continue;
-                        uint32_t ppc = uni(tr.ordpc[ordc]);
+                        uint32_t ppc = uni(ordpc[ordc]);
                         uint32_t count = uni(prog[ppc].u0);
                         Ivl iv = prim_interval(prog, ppc, count, o, d);
                         if (!(iv.a > iv.b)) {
@@ -398,23 +236,9 @@ __device__ __forceinline__ bool trace(Prog prog, uint32_t nrec, Trace& tr, F3 o,
                 }
             }
         }
-        break;
+        return false;
     }
-    return found;
-}
-
-__device__ __forceinline__ F3 sky(F3 d) {
-    float t = 0.5f * (d.y + 1.0f);
-    float s = 1.0f - t;
-    return f3(s + t * 0.5f, s + t * 0.7f, s + t * 1.0f);
-}
-
-// Pixel -> (local row) mapping for row-cyclic rank tiles.
-__device__ __forceinline__ uint32_t local_to_global_row(const WoFrame& fr, uint32_t lrow) {
-    uint32_t lt = lrow / fr.tile_rows;
-    uint32_t g = lt * fr.nranks + fr.rank;
-    return g * fr.tile_rows + (lrow - lt * fr.tile_rows);
-}
+};
 
 // ---------------------------------------------------------------------------
 // ubershader1.frag restated (ref ubershader1.frag:19-163).
@@ -427,13 +251,13 @@ __global__ __launch_bounds__(kBlock) void ubershader_kernel(WoFrame fr, uint32_t
     if (y >= fr.height) return;
 
     float resx = (float)fr.width, resy = (float)fr.height;
-    float aspect = resx / resy;                   // frag:20
-    float fx = (float)lx + 0.5f;                  // gl_FragCoord at the pixel centre,
-    float fy = (float)y + 0.5f;                   // OriginUpperLeft (row 0 = top)
-    float stx = fx / resx;                        // frag:26-29
+    float aspect = resx / resy;   // frag:20
+    float fx = (float)lx + 0.5f;  // gl_FragCoord at the pixel centre,
+    float fy = (float)y + 0.5f;   // OriginUpperLeft (row 0 = top)
+    float stx = fx / resx;        // frag:26-29
     float sty = 1.0f - fy / resy;
     float4 res;
-    if (fr.mode == WO_MODE_DEBUG_ST) {            // frag:133-138
+    if (fr.mode == WO_MODE_DEBUG_ST) {  // frag:133-138
         res = make_float4(stx, sty, 0.0f, 1.0f);
     } else {
         // camera (frag:50-60): llc = (-aspect/2, -0.5, -1); ray dir (frag:74-82), not normalised
@@ -467,14 +291,6 @@ __global__ __launch_bounds__(kBlock) void ubershader_kernel(WoFrame fr, uint32_t
     out[(size_t)lrow * fr.width + lx] = res;
 }
 
-// ---------------------------------------------------------------------------
-// CSG path tracer.
-// ---------------------------------------------------------------------------
-struct ProgPtr {
-    const WoRec* p;
-    __device__ __forceinline__ WoRec operator[](uint32_t i) const { return p[i]; }
-};
-
 template <bool kProgInLds>
 __global__ __launch_bounds__(kBlock) void pathtrace_kernel(const WoRec* __restrict__ gprog,
                                                            const WoMaterial* __restrict__ mats, WoFrame fr,
@@ -486,185 +302,26 @@ __global__ __launch_bounds__(kBlock) void pathtrace_kernel(const WoRec* __restri
     const uint32_t nrec = fr.n_recs;
 
     uint32_t* scratch = smem;
-    ProgPtr prog;
+    InterpTracer tr;
     if constexpr (kProgInLds) {
         const uint4* src = reinterpret_cast<const uint4*>(gprog);
         uint4* dst = reinterpret_cast<uint4*>(smem);
         for (uint32_t i = tid; i < nrec * 2u; i += kBlock) dst[i] = src[i];
         __syncthreads();
-        prog.p = reinterpret_cast<const WoRec*>(smem);
+        tr.prog.p = reinterpret_cast<const WoRec*>(smem);
         scratch = smem + nrec * 8u;
     } else {
-        prog.p = gprog;
+        tr.prog.p = gprog;
     }
     uint32_t* ws = scratch + wave * lay.wave_words;
-    Trace tr;
+    tr.nrec = nrec;
     tr.codes = ws;
     tr.ordpc = ws + lay.ordpc_off;
     tr.hib = ws + lay.hib_off;
     tr.lane = lane;
-
-    // 16x16 block; each wave an 8x8 pixel tile for ray coherence.
-    uint32_t lx = blockIdx.x * kPtTile + (wave & 1u) * 8u + (lane & 7u);
-    uint32_t lrow = blockIdx.y * kPtTile + (wave >> 1) * 8u + (lane >> 3);
-    uint32_t y = lrow < local_rows ? local_to_global_row(fr, lrow) : fr.height;
-    bool active = lx < fr.width && y < fr.height;
-
-    const WoCamera& cam = fr.cam;
-    const uint32_t W = fr.width, H = fr.height;
-    const uint32_t pix = y * W + lx;
-    const uint32_t spp = fr.mode == WO_MODE_NORMALS ? 1u : fr.spp;
-    const uint32_t max_depth = fr.mode == WO_MODE_NORMALS ? 1u : fr.max_depth;
-    const uint32_t seed_hash = pcg_hash(fr.seed);
-
-    F3 acc = f3(0.0f, 0.0f, 0.0f);
-    F3 o = f3(0.0f, 0.0f, 0.0f), d = f3(0.0f, 0.0f, -1.0f), thr = f3(1.0f, 1.0f, 1.0f);
-    Rng rng;
-    rng.s = 0;
-    uint32_t sample = 0, depth = 0;
-    uint32_t segs = 0;
-    bool done = !active || spp == 0u || max_depth == 0u;
-
-    // Camera ray for (pix, sample); RTIOW camera.get_ray with defocus.
-    auto start_sample = [&]() {
-        rng.s = pcg_hash(pix ^ pcg_hash((fr.sample_offset + sample) ^ seed_hash));
-        float sx, ty;
-        if (fr.mode == WO_MODE_NORMALS) {
-            sx = ((float)lx + 0.5f) / (float)W;
-            ty = ((float)(H - 1u - y) + 0.5f) / (float)H;
-        } else {
-            float r1 = rng.uniform();
-            float r2 = rng.uniform();
-            sx = ((float)lx + r1) / (float)W;
-            ty = ((float)(H - 1u - y) + r2) / (float)H;
-        }
-        float offx = 0.0f, offy = 0.0f, offz = 0.0f;
-        if (cam.lens_radius > 0.0f && fr.mode != WO_MODE_NORMALS) {
-            float px = 0.0f, py = 0.0f;
-            for (int i = 0; i < 64; ++i) {
-                px = 2.0f * rng.uniform() - 1.0f;
-                py = 2.0f * rng.uniform() - 1.0f;
-                if (px * px + py * py < 1.0f) break;
-            }
-            float rx = cam.lens_radius * px, ry = cam.lens_radius * py;
-            offx = cam.u[0] * rx + cam.v[0] * ry;
-            offy = cam.u[1] * rx + cam.v[1] * ry;
-            offz = cam.u[2] * rx + cam.v[2] * ry;
-        }
-        o = f3(cam.origin[0] + offx, cam.origin[1] + offy, cam.origin[2] + offz);
-        F3 dir = f3(((cam.lower_left[0] + sx * cam.horizontal[0]) + ty * cam.vertical[0]) - cam.origin[0] - offx,
-                    ((cam.lower_left[1] + sx * cam.horizontal[1]) + ty * cam.vertical[1]) - cam.origin[1] - offy,
-                    ((cam.lower_left[2] + sx * cam.horizontal[2]) + ty * cam.vertical[2]) - cam.origin[2] - offz);
-        d = unit3(dir);
-        thr = f3(1.0f, 1.0f, 1.0f);
-        depth = 0;
-    };
-    if (!done) start_sample();
-
-    while (__any(!done)) {
-        if (!done) {
-            Hit h;
-            bool found = trace(prog, nrec, tr, o, d, h);
-            ++segs;
-            bool end = false;
-            F3 radiance = f3(0.0f, 0.0f, 0.0f);
-            if (!found) {
-                F3 s = sky(d);
-                radiance = f3(thr.x * s.x, thr.y * s.y, thr.z * s.z);
-                end = true;
-            } else {
-                uint32_t ppc = tr.ordpc[h.ord];
-                WoRec L = prog[ppc + 1u + h.member];
-                F3 P = f3(o.x + h.t * d.x, o.y + h.t * d.y, o.z + h.t * d.z);
-                F3 n;
-                if (L.op == WO_LEAF_SPHERE)
-                    n = f3((P.x - L.f[0]) * L.f[4], (P.y - L.f[1]) * L.f[4], (P.z - L.f[2]) * L.f[4]);
-                else
-                    n = f3(L.f[0], L.f[1], L.f[2]);
-                // Leaf entered (type 0): its outward normal faces the ray.
-                F3 N = h.type == 0u ? n : f3(-n.x, -n.y, -n.z);
-                bool front = h.root_after != 0u;
-                if (fr.mode == WO_MODE_NORMALS) {
-                    // outward normal of the solid
-                    F3 ns = front ? N : f3(-N.x, -N.y, -N.z);
-                    radiance = f3(0.5f * (ns.x + 1.0f), 0.5f * (ns.y + 1.0f), 0.5f * (ns.z + 1.0f));
-                    end = true;
-                } else {
-                    const WoMaterial m = mats[L.u0];
-                    F3 nd;
-                    F3 att;
-                    bool scatter = true;
-                    if (m.kind == WO_MAT_LAMBERTIAN) {
-                        F3 ru = unit3(random_in_unit_sphere(rng));
-                        F3 sd = f3(N.x + ru.x, N.y + ru.y, N.z + ru.z);
-                        if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = N;
-                        nd = unit3(sd);
-                        att = f3(m.albedo[0], m.albedo[1], m.albedo[2]);
-                    } else if (m.kind == WO_MAT_METAL) {
-                        float k = 2.0f * dot3(d, N);
-                        F3 rs = random_in_unit_sphere(rng);
-                        F3 sc = f3((d.x - k * N.x) + m.fuzz * rs.x, (d.y - k * N.y) + m.fuzz * rs.y,
-                                   (d.z - k * N.z) + m.fuzz * rs.z);
-                        scatter = dot3(sc, N) > 0.0f;
-                        nd = unit3(sc);
-                        att = f3(m.albedo[0], m.albedo[1], m.albedo[2]);
-                    } else {
-                        float ri = front ? (1.0f / m.ior) : m.ior;
-                        float ct = dot3(f3(-d.x, -d.y, -d.z), N);
-                        ct = ct < 1.0f ? ct : 1.0f;
-                        float st = sqrtf(1.0f - ct * ct);
-                        bool reflect = ri * st > 1.0f;
-                        if (!reflect) {
-                            float r0 = (1.0f - ri) / (1.0f + ri);
-                            r0 = r0 * r0;
-                            float x = 1.0f - ct;
-                            float x5 = (((x * x) * x) * x) * x;
-                            float refl = r0 + (1.0f - r0) * x5;
-                            reflect = refl > rng.uniform();
-                        }
-                        F3 sc;
-                        if (reflect) {
-                            float k = 2.0f * dot3(d, N);
-                            sc = f3(d.x - k * N.x, d.y - k * N.y, d.z - k * N.z);
-                        } else {
-                            F3 perp = f3(ri * (d.x + ct * N.x), ri * (d.y + ct * N.y), ri * (d.z + ct * N.z));
-                            float par = -sqrtf(fabsf(1.0f - dot3(perp, perp)));
-                            sc = f3(perp.x + par * N.x, perp.y + par * N.y, perp.z + par * N.z);
-                        }
-                        nd = unit3(sc);
-                        att = f3(1.0f, 1.0f, 1.0f);
-                    }
-                    if (!scatter) {
-                        end = true;
-                    } else {
-                        thr = f3(thr.x * att.x, thr.y * att.y, thr.z * att.z);
-                        o = P;
-                        d = nd;
-                        ++depth;
-                        if (depth >= max_depth) end = true;
-                    }
-                }
-            }
-            if (end) {
-                acc = f3(acc.x + radiance.x, acc.y + radiance.y, acc.z + radiance.z);
-                ++sample;
-                if (sample >= spp)
-                    done = true;
-                else
-                    start_sample();
-            }
-        }
-    }
-
-    if (active) {
-        float fs = (float)spp;
-        out[(size_t)lrow * W + lx] = make_float4(acc.x / fs, acc.y / fs, acc.z / fs, 1.0f);
-    }
-    if (seg_out != nullptr) {
-        unsigned long long v = segs;
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (lane == 0u && v != 0ull) atomicAdd(seg_out, v);
-    }
+    uint32_t lx, lrow;
+    block_pixel(tid, lx, lrow);
+    pathtrace_pixel(tr, mats, fr, lx, lrow, local_rows, out, seg_out, lane);
 }
 
 __global__ __launch_bounds__(kBlock) void assemble_kernel(const float4* __restrict__ gathered, float4* __restrict__ frame,
@@ -687,6 +344,7 @@ __global__ __launch_bounds__(kBlock) void assemble_kernel(const float4* __restri
 // ===========================================================================
 struct WoDev {
     int device;
+    std::string arch;  // gcnArchName, e.g. gfx950:sramecc+:xnack-
     WoRec* d_prog;
     size_t prog_cap;
     WoMaterial* d_mats;
@@ -695,6 +353,11 @@ struct WoDev {
     float4* d_frame;
     size_t frame_cap;
     hipStream_t stream;
+    // scene-specialised kernel (hiprtc)
+    hipModule_t jit_module;
+    hipFunction_t jit_fn;
+    uint64_t jit_hash;
+    double jit_compile_sec;
 };
 
 static void set_err(char* err, size_t len, const char* what, hipError_t e) {
@@ -719,16 +382,23 @@ extern "C" int wo_dev_create(int device, WoDev** out, char* err, size_t errlen) 
         set_err(err, errlen, "hipSetDevice", e);
         return -1;
     }
-    WoDev* dev = (WoDev*)calloc(1, sizeof(WoDev));
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipGetDeviceProperties", e);
+        return -1;
+    }
+    WoDev* dev = new (std::nothrow) WoDev();
     if (!dev) {
         snprintf(err, errlen, "out of host memory");
         return -1;
     }
     dev->device = device;
+    dev->arch = prop.gcnArchName;
     e = hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         set_err(err, errlen, "hipStreamCreate", e);
-        free(dev);
+        delete dev;
         return -1;
     }
     *out = dev;
@@ -742,8 +412,9 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
     if (dev->d_prog) (void)hipFree(dev->d_prog);
     if (dev->d_mats) (void)hipFree(dev->d_mats);
     if (dev->d_frame) (void)hipFree(dev->d_frame);
+    if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
     (void)hipStreamDestroy(dev->stream);
-    free(dev);
+    delete dev;
 }
 
 template <class T>
@@ -791,6 +462,104 @@ extern "C" int wo_dev_upload_scene(WoDev* dev, WoRec const* prog, uint32_t n_rec
     return 0;
 }
 
+// ---- scene-specialised kernels (hiprtc) ----
+
+static uint64_t fnv1a(const char* s, size_t n, uint64_t h = 1469598103934665603ull) {
+    for (size_t i = 0; i < n; ++i) h = (h ^ (unsigned char)s[i]) * 1099511628211ull;
+    return h;
+}
+
+// Process-wide cache of compiled code objects (the same scene compiled once).
+static std::mutex g_jit_mu;
+static std::unordered_map<uint64_t, std::vector<char>>& jit_cache() {
+    static std::unordered_map<uint64_t, std::vector<char>> m;
+    return m;
+}
+
+static int jit_compile(const char* src, const std::string& arch, std::vector<char>& code, char* err, size_t errlen) {
+    hiprtcProgram p;
+    const char* hdr_src[] = {kEmbed_wo_device_common_h, kEmbed_wo_scene_h};
+    const char* hdr_names[] = {"wo_device_common.h", "wololo/wo_scene.h"};
+    if (hiprtcCreateProgram(&p, src, "wo_scene_jit.hip", 2, hdr_src, hdr_names) != HIPRTC_SUCCESS) {
+        snprintf(err, errlen, "hiprtcCreateProgram failed");
+        return -1;
+    }
+    std::string arch_opt = "--offload-arch=" + arch;
+    const char* opts[] = {arch_opt.c_str(), "-O3", "-ffp-contract=off", "-std=c++17"};
+    hiprtcResult rc = hiprtcCompileProgram(p, 4, opts);
+    if (rc != HIPRTC_SUCCESS) {
+        size_t ls = 0;
+        hiprtcGetProgramLogSize(p, &ls);
+        std::string log(ls + 1, '\0');
+        hiprtcGetProgramLog(p, &log[0]);
+        snprintf(err, errlen, "hiprtc: %s: %.400s", hiprtcGetErrorString(rc), log.c_str());
+        hiprtcDestroyProgram(&p);
+        return -1;
+    }
+    size_t cs = 0;
+    hiprtcGetCodeSize(p, &cs);
+    code.resize(cs);
+    hiprtcGetCode(p, code.data());
+    hiprtcDestroyProgram(&p);
+    return 0;
+}
+
+extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t errlen) {
+    hipError_t e = hipSetDevice(dev->device);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipSetDevice", e);
+        return -1;
+    }
+    if (!src) {  // disable
+        if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
+        dev->jit_module = nullptr;
+        dev->jit_fn = nullptr;
+        dev->jit_hash = 0;
+        return 0;
+    }
+    uint64_t h = fnv1a(dev->arch.data(), dev->arch.size(), fnv1a(src, strlen(src)));
+    if (dev->jit_fn && dev->jit_hash == h) return 0;
+    std::vector<char> code;
+    {
+        std::lock_guard<std::mutex> lock(g_jit_mu);
+        auto it = jit_cache().find(h);
+        if (it != jit_cache().end()) code = it->second;
+    }
+    if (code.empty()) {
+        auto t0 = std::chrono::steady_clock::now();
+        if (jit_compile(src, dev->arch, code, err, errlen)) return -1;
+        dev->jit_compile_sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::lock_guard<std::mutex> lock(g_jit_mu);
+        jit_cache()[h] = code;
+    }
+    hipModule_t mod = nullptr;
+    e = hipModuleLoadData(&mod, code.data());
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipModuleLoadData", e);
+        return -1;
+    }
+    hipFunction_t fn = nullptr;
+    e = hipModuleGetFunction(&fn, mod, "wo_jit_pathtrace");
+    if (e != hipSuccess) {
+        (void)hipModuleUnload(mod);
+        set_err(err, errlen, "hipModuleGetFunction", e);
+        return -1;
+    }
+    if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
+    dev->jit_module = mod;
+    dev->jit_fn = fn;
+    dev->jit_hash = h;
+    return 0;
+}
+
+extern "C" int wo_jit_compile_check(const char* src, const char* arch, char* err, size_t errlen) {
+    std::vector<char> code;
+    return jit_compile(src, arch ? std::string(arch) : std::string("gfx950"), code, err, errlen);
+}
+
+extern "C" int wo_dev_jit_active(WoDev* dev) { return dev && dev->jit_fn ? 1 : 0; }
+extern "C" double wo_dev_jit_compile_sec(WoDev* dev) { return dev ? dev->jit_compile_sec : 0.0; }
+
 static const size_t kLdsBudget = 64u * 1024u;
 
 extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, void* stream_v,
@@ -822,24 +591,36 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
             snprintf(err, errlen, "scene has %u primitives (max %u)", fr.n_prims, (1u << 20) - 1u);
             return -1;
         }
-        KLayout lay;
-        lay.codes_words = (fr.n_recs + 7u) / 8u + 1u;
-        lay.ordpc_off = lay.codes_words;
-        uint32_t hib_words = fr.n_prims > 64u ? (fr.n_prims - 64u + 31u) / 32u : 0u;
-        lay.hib_off = lay.ordpc_off + fr.n_prims;
-        lay.wave_words = (lay.hib_off + hib_words * 64u + 3u) & ~3u;
-        size_t scratch = (size_t)(kBlock / 64u) * lay.wave_words * 4u;
-        size_t prog_bytes = (size_t)fr.n_recs * sizeof(WoRec);
         dim3 grid((fr.width + kPtTile - 1) / kPtTile, (local_rows + kPtTile - 1) / kPtTile);
-        if (prog_bytes + scratch <= kLdsBudget) {
-            hipLaunchKernelGGL(pathtrace_kernel<true>, grid, dim3(kBlock), prog_bytes + scratch, stream, dev->d_prog,
-                               dev->d_mats, fr, lay, local_rows, out, d_segments);
-        } else if (scratch <= kLdsBudget) {
-            hipLaunchKernelGGL(pathtrace_kernel<false>, grid, dim3(kBlock), scratch, stream, dev->d_prog, dev->d_mats,
-                               fr, lay, local_rows, out, d_segments);
+        if (dev->jit_fn) {
+            const WoRec* p = dev->d_prog;
+            const WoMaterial* m = dev->d_mats;
+            unsigned long long* s = d_segments;
+            void* args[] = {&p, &m, &fr, &local_rows, &out, &s};
+            e = hipModuleLaunchKernel(dev->jit_fn, grid.x, grid.y, 1, kBlock, 1, 1, 0, stream, args, nullptr);
+            if (e != hipSuccess) {
+                set_err(err, errlen, "hipModuleLaunchKernel", e);
+                return -1;
+            }
         } else {
-            snprintf(err, errlen, "scene too large for the LDS scratch (%zu bytes per workgroup)", scratch);
-            return -1;
+            KLayout lay;
+            lay.codes_words = (fr.n_recs + 7u) / 8u + 1u;
+            lay.ordpc_off = lay.codes_words;
+            uint32_t hib_words = fr.n_prims > 64u ? (fr.n_prims - 64u + 31u) / 32u : 0u;
+            lay.hib_off = lay.ordpc_off + fr.n_prims;
+            lay.wave_words = (lay.hib_off + hib_words * 64u + 3u) & ~3u;
+            size_t scratch = (size_t)(kBlock / 64u) * lay.wave_words * 4u;
+            size_t prog_bytes = (size_t)fr.n_recs * sizeof(WoRec);
+            if (prog_bytes + scratch <= kLdsBudget) {
+                hipLaunchKernelGGL(pathtrace_kernel<true>, grid, dim3(kBlock), prog_bytes + scratch, stream,
+                                   dev->d_prog, dev->d_mats, fr, lay, local_rows, out, d_segments);
+            } else if (scratch <= kLdsBudget) {
+                hipLaunchKernelGGL(pathtrace_kernel<false>, grid, dim3(kBlock), scratch, stream, dev->d_prog,
+                                   dev->d_mats, fr, lay, local_rows, out, d_segments);
+            } else {
+                snprintf(err, errlen, "scene too large for the LDS scratch (%zu bytes per workgroup)", scratch);
+                return -1;
+            }
         }
     } else {
         snprintf(err, errlen, "unknown shading mode %u", fr.mode);

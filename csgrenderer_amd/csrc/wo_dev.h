@@ -28,6 +28,12 @@ void wo_dev_destroy(WoDev* dev);
 /* Copy the compiled scene to HBM (blocking). */
 int wo_dev_upload_scene(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n_prims,
                         WoMaterial const* mats, uint32_t n_mats, char* err, size_t errlen);
+/* Compile (hiprtc, cached per process) and load a scene-specialised path
+ * tracer from `src` (scene_jit.c); NULL unloads it.  While loaded, PATHTRACE and
+ * NORMALS frames launch it instead of the interpreter kernel. */
+int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t errlen);
+int wo_dev_jit_active(WoDev* dev);
+double wo_dev_jit_compile_sec(WoDev* dev);
 /* Launch the frame's kernel for this rank's tiles into d_out on `stream` (async). */
 int wo_dev_launch(WoDev* dev, WoFrame const* frame, void* d_out, void* stream,
                   unsigned long long* d_segments, char* err, size_t errlen);

@@ -66,6 +66,9 @@ struct Wo_Renderer {
     int device;         /* -1: device-less (tests only) */
     WoDev* dev;
 
+    int jit_mode;       /* 0 off, 1 auto (scenes up to WOLOLO_JIT_MAX_PRIMS primitives) */
+    int jit_loaded;     /* the device runs the scene-specialised kernel */
+
     float* host_frame;
     size_t host_frame_cap;
     uint64_t frames_drawn;
@@ -74,6 +77,9 @@ struct Wo_Renderer {
 /* scene_compile.c */
 int wo_compile_scene(Wo_Renderer* r, char* err, size_t errlen);
 void wo_resolve_camera(WoCameraDesc const* desc, uint32_t width, uint32_t height, WoCamera* out);
+
+/* scene_jit.c: HIP source of the scene-specialised trace kernel (malloc'd) */
+char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prims);
 
 /* renderer.c */
 void wo_set_error(char const* fmt, ...);

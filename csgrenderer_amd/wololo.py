@@ -108,6 +108,11 @@ SIGNATURES = {
     "wo_renderer_materials": (POINTER(WoMaterial), [c_void_p, POINTER(c_uint32)]),
     "wo_renderer_frame_desc": (c_int, [c_void_p, POINTER(RenderParams), c_uint32, c_uint32, c_uint32,
                                        POINTER(WoFrame)]),
+    "wo_renderer_set_jit": (None, [c_void_p, c_int]),
+    "wo_renderer_trace_path": (c_char_p, [c_void_p]),
+    "wo_renderer_jit_source": (c_void_p, [c_void_p]),
+    "wo_jit_compile_check": (c_int, [c_char_p, c_char_p, c_char_p, c_size_t]),
+    "wo_free": (None, [c_void_p]),
     "wo_renderer_node_count": (c_size_t, [c_void_p]),
     "wo_renderer_name": (c_char_p, [c_void_p]),
     "wo_renderer_device": (c_int, [c_void_p]),
@@ -245,6 +250,21 @@ class Renderer:
         ctypes.memmove(arr, p, ctypes.sizeof(WoMaterial) * n.value)
         return arr, n.value
 
+    def jit_source(self) -> str | None:
+        p = self.lib.wo_renderer_jit_source(self.ptr)
+        if not p:
+            return None
+        try:
+            return ctypes.string_at(p).decode()
+        finally:
+            self.lib.wo_free(p)
+
+    def set_jit(self, mode: int):
+        self.lib.wo_renderer_set_jit(self.ptr, int(mode))
+
+    def trace_path(self) -> str:
+        return self.lib.wo_renderer_trace_path(self.ptr).decode()
+
     def frame_desc(self, params: RenderParams, tile_rows=16, rank=0, nranks=1) -> WoFrame:
         fr = WoFrame()
         if self.lib.wo_renderer_frame_desc(self.ptr, ctypes.byref(params), tile_rows, rank, nranks,
@@ -279,6 +299,13 @@ def assemble_rows_device(d_gathered: int, d_frame: int, width: int, height: int,
     if lib.wo_assemble_rows_device(c_void_p(d_gathered), c_void_p(d_frame), width, height, tile_rows, nranks,
                                    c_void_p(stream or None)):
         raise WololoError(last_error())
+
+
+def jit_compile_check(src: str, arch: str = "gfx950") -> str:
+    """Compile generated source with hiprtc (no GPU needed); '' on success, else the log."""
+    err = ctypes.create_string_buffer(4096)
+    rc = load().wo_jit_compile_check(src.encode(), arch.encode(), err, len(err))
+    return "" if rc == 0 else err.value.decode(errors="replace")
 
 
 def local_rows(height: int, tile_rows: int, nranks: int) -> int:

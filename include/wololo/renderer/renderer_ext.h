@@ -89,6 +89,22 @@ WoMaterial const* wo_renderer_materials(Wo_Renderer* r, uint32_t* n_materials);
 int wo_renderer_frame_desc(Wo_Renderer* r, Wo_RenderParams const* params, uint32_t tile_rows,
                            uint32_t rank, uint32_t nranks, WoFrame* out);
 
+/* Scene-specialised kernels: 0 = always use the interpreter kernel, 1 = auto
+ * (default: specialise scenes of up to WOLOLO_JIT_MAX_PRIMS primitives, default
+ * 256, compiled with hiprtc at scene upload; WOLOLO_JIT=0 in the environment
+ * turns it off).  Takes effect at the next render. */
+void wo_renderer_set_jit(Wo_Renderer* r, int mode);
+/* Which path kernel the last render used: "jit", "interpreter" or "none". */
+char const* wo_renderer_trace_path(Wo_Renderer* r);
+
+/* HIP source of the scene-specialised kernel for the current scene (NULL if
+ * the scene has no primitives); release with wo_free(). */
+char* wo_renderer_jit_source(Wo_Renderer* r);
+/* Compile `src` with hiprtc for `arch` (e.g. "gfx950") without loading it --
+ * needs no GPU.  Returns 0, or -1 with the compiler log in err. */
+int wo_jit_compile_check(char const* src, char const* arch, char* err, size_t errlen);
+void wo_free(void* p);
+
 size_t wo_renderer_node_count(Wo_Renderer* r);
 char const* wo_renderer_name(Wo_Renderer* r);
 /* HIP device ordinal the renderer runs on; -1 for a device-less renderer. */

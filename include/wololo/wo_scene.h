@@ -26,7 +26,12 @@
 #ifndef WOLOLO_WO_SCENE_H
 #define WOLOLO_WO_SCENE_H
 
+#if defined(__HIPCC_RTC__) /* hiprtc: no libc headers; take its internal fixed-width types */
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::uint64_t uint64_t;
+#else
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {

@@ -69,10 +69,21 @@ def test_ubershader_kats_on_gpu(empty_renderer):
     assert hits == kats["hit_pixels_256_t0"]
 
 
-def _scene(name, **kw):
+PATHS = ["jit", "interpreter"]
+
+
+def _scene(name, path="jit", **kw):
     r = wl.Renderer(name, max_nodes=4096)
     info = scenes.build(name, r, **kw) if name in scenes.SCENES else None
+    r.set_jit(1 if path == "jit" else 0)
     return r, info
+
+
+def _check_path(r, path, scene=None):
+    want = path
+    if path == "jit" and scene == "rtiow_cover":
+        want = "interpreter"  # 487 primitives > WOLOLO_JIT_MAX_PRIMS: stays on the interpreter
+    assert r.trace_path() == want, (r.trace_path(), want)
 
 
 def _oracle_rows(r, params):
@@ -83,22 +94,25 @@ def _oracle_rows(r, params):
     return img, segs
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("scene", ["csg32", "rtiow_cover", "csg256_balanced", "csg256_chain"])
 @pytest.mark.parametrize("mode", [wl.MODE_PATHTRACE, wl.MODE_NORMALS])
-def test_pathtrace_small_frame_bitexact(scene, mode):
-    r, info = _scene(scene)
+def test_pathtrace_small_frame_bitexact(scene, mode, path):
+    r, info = _scene(scene, path)
     p = info.params(width=96, height=54, spp=8 if mode == wl.MODE_PATHTRACE else 1, mode=mode, seed=7)
     img = r.render(p)
+    _check_path(r, path, scene)
     ref, _ = _oracle_rows(r, p)
-    _cmp(img, ref, f"{scene} mode={mode}")
+    _cmp(img, ref, f"{scene} mode={mode} path={path}")
     r.close()
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("scene", ["csg32", "rtiow_cover", "csg256_balanced"])
-def test_pathtrace_full_size_sampled_pixels(scene):
+def test_pathtrace_full_size_sampled_pixels(scene, path):
     """BASELINE configs at full size (1920x1080, 64 spp, 8 bounces): the whole frame on
     the GPU, a random sample of pixels on the oracle."""
-    r, info = _scene(scene)
+    r, info = _scene(scene, path)
     p = info.params()
     img = r.render(p)
     assert np.isfinite(img).all()
@@ -113,10 +127,11 @@ def test_pathtrace_full_size_sampled_pixels(scene):
     r.close()
 
 
-def test_golden_fixtures_on_gpu():
+@pytest.mark.parametrize("path", PATHS)
+def test_golden_fixtures_on_gpu(path):
     man = json.load(open(os.path.join(GOLD, "manifest.json")))
     for case in man["pathtrace"]:
-        r, info = _scene(case["scene"])
+        r, info = _scene(case["scene"], path)
         p = info.params(width=case["w"], height=case["h"], spp=case["spp"], mode=case["mode"])
         img = r.render(p)
         ref = np.fromfile(os.path.join(GOLD, case["file"]), dtype=np.float32).reshape(case["h"], case["w"], 4)
@@ -152,10 +167,11 @@ def _torch():
     return torch
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("nranks,tile", [(1, 16), (2, 16), (3, 8), (8, 16), (5, 7)])
-def test_row_tiles_assemble_to_full_frame(nranks, tile):
+def test_row_tiles_assemble_to_full_frame(nranks, tile, path):
     torch = _torch()
-    r, info = _scene("csg32")
+    r, info = _scene("csg32", path)
     p = info.params(width=200, height=123, spp=2)
     full = r.render(p)
     lr = wl.local_rows(p.height, tile, nranks)
@@ -174,9 +190,11 @@ def test_row_tiles_assemble_to_full_frame(nranks, tile):
     r.close()
 
 
-def test_event_window_overflow_restart():
+@pytest.mark.parametrize("path", PATHS)
+def test_event_window_overflow_restart(path):
     """A ray crossing > 8 primitive boundaries exercises the window re-collection path."""
     r = wl.Renderer("overflow", max_nodes=256)
+    r.set_jit(1 if path == "jit" else 0)
     items = []
     for i in range(24):  # a row of overlapping spheres along -z in front of the camera
         s = r.sphere(0.6)
@@ -191,14 +209,17 @@ def test_event_window_overflow_restart():
     for mode, spp in [(wl.MODE_NORMALS, 1), (wl.MODE_PATHTRACE, 4)]:
         p = wl.render_params(48, 48, spp=spp, max_depth=6, mode=mode)
         img = r.render(p)
+        _check_path(r, path)
         ref, _ = _oracle_rows(r, p)
-        _cmp(img, ref, f"overflow mode={mode}")
+        _cmp(img, ref, f"overflow mode={mode} path={path}")
     r.close()
 
 
-def test_edge_scenes():
+@pytest.mark.parametrize("path", PATHS)
+def test_edge_scenes(path):
     # empty scene: sky only
     r = wl.Renderer("empty", max_nodes=4)
+    r.set_jit(1 if path == "jit" else 0)
     p = wl.render_params(32, 16, spp=2, mode=wl.MODE_PATHTRACE)
     img = r.render(p)
     ref, segs = _oracle_rows(r, p)
@@ -207,6 +228,7 @@ def test_edge_scenes():
     r.close()
     # a lone ground half-space (unbounded), a zero-radius sphere, a degenerate normal
     r = wl.Renderer("edges", max_nodes=16)
+    r.set_jit(1 if path == "jit" else 0)
     g = r.halfspace((0, 1, 0))
     z = r.sphere(0.0)
     dgn = r.halfspace((0, 0, 0))
@@ -219,8 +241,9 @@ def test_edge_scenes():
     for mode, spp in [(wl.MODE_NORMALS, 1), (wl.MODE_PATHTRACE, 4)]:
         p = wl.render_params(64, 48, spp=spp, max_depth=8, mode=mode)
         img = r.render(p)
+        _check_path(r, path)
         ref, _ = _oracle_rows(r, p)
-        _cmp(img, ref, f"edge scene mode={mode}")
+        _cmp(img, ref, f"edge scene mode={mode} path={path}")
     r.close()
 
 

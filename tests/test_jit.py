@@ -1,0 +1,53 @@
+"""Scene-specialised kernels (csrc/scene_jit.c): the generated HIP source compiles
+for gfx950 with hiprtc (no GPU needed) and mirrors the compiled program (CPU)."""
+import re
+
+import numpy as np
+import pytest
+
+from csgrenderer_amd import scenes
+from csgrenderer_amd import wololo as wl
+
+
+def test_csg32_source_compiles_for_gfx950(hostonly):
+    r = wl.Renderer("jit", max_nodes=4096)
+    scenes.build("csg32", r)
+    prog, nrec, nprim = r.program()
+    src = r.jit_source()
+    assert src is not None
+    # one intersection call per leaf, one cull flag per BOUND, ordinal table of every primitive
+    nleaf = sum(1 for i in range(nrec) if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE))
+    assert len(re.findall(r"wodev::(sphere|halfspace)_interval\(", src)) == nleaf
+    nb = sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND)
+    assert len(re.findall(r"if \(first\) c\d+ = __ballot", src)) == nb
+    m = re.search(r"kOrdPc\[(\d+)\] = \{([^}]*)\}", src)
+    assert int(m.group(1)) == nprim
+    pcs = [int(x.strip().rstrip("u")) for x in m.group(2).split(",")]
+    assert pcs == [i for i in range(nrec) if prog[i].op == wl.WO_OP_PRIM]
+    log = wl.jit_compile_check(src, "gfx950")
+    assert log == "", log
+    r.close()
+
+
+def test_literals_round_trip(hostonly):
+    """Leaf parameters are emitted as hex-float literals that round-trip exactly."""
+    r = wl.Renderer("lit", max_nodes=8)
+    s = r.sphere(0.1)
+    h = r.halfspace((0.3, -0.7, 0.2))
+    r.union(wl.arg(s, (1.0 / 3.0, 2.0 / 7.0, -1e-7)), wl.arg(h, (0.1, 0.2, 0.3)))
+    prog, nrec, _ = r.program()
+    src = r.jit_source()
+    lits = [float.fromhex(x) for x in re.findall(r"(-?0x[0-9a-f.]+p[-+]\d+)f", src)]
+    for i in range(nrec):
+        if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE):
+            for k in range(4):
+                v = prog[i].f[k]
+                assert any(np.float32(x) == np.float32(v) for x in lits), v
+    assert wl.jit_compile_check(src) == ""
+    r.close()
+
+
+def test_empty_scene_has_no_source(hostonly):
+    r = wl.Renderer("e", max_nodes=2)
+    assert r.jit_source() is None
+    r.close()
