@@ -56,17 +56,25 @@ static void bput(Buf* b, const char* fmt, ...) {
     }
 }
 
-/* fp32 literal that round-trips exactly */
-static void flit(char out[48], float v) {
-    if (v != v) {
-        snprintf(out, 48, "__builtin_nanf(\"\")");
-    } else if (v == __builtin_inff()) {
-        snprintf(out, 48, "wodev::kInf");
-    } else if (v == -__builtin_inff()) {
-        snprintf(out, 48, "(-wodev::kInf)");
-    } else {
-        snprintf(out, 48, "%af", (double)v);
-    }
+static uint32_t fbits(float v) {
+    uint32_t u;
+    memcpy(&u, &v, sizeof u);
+    return u;
+}
+
+/* Scene constants are materialised by a volatile s_mov_b32 AT THEIR USE: every
+ * trace runs inside the sample loop, and plain literals are loop-invariant, so
+ * the compiler would hoist hundreds of them into registers for the whole kernel
+ * (measured: 210 VGPRs, 160 SGPR spills for csg32).  One SALU op per constant
+ * keeps them in short-lived SGPRs.  `names` are the declared float variables. */
+static void emit_consts(Buf* b, int indent, const char* type, const char* names[], const uint32_t* vals, int n) {
+    bput(b, "%*s%s %s", indent, "", type, names[0]);
+    for (int i = 1; i < n; ++i) bput(b, ", %s", names[i]);
+    bput(b, ";\n%*sasm volatile(\"", indent, "");
+    for (int i = 0; i < n; ++i) bput(b, "%ss_mov_b32 %%%d, 0x%08x", i ? "\\n\\t" : "", i, vals[i]);
+    bput(b, "\" : ");
+    for (int i = 0; i < n; ++i) bput(b, "%s\"=s\"(%s)", i ? ", " : "", names[i]);
+    bput(b, ");\n");
 }
 
 typedef struct Gen {
@@ -84,43 +92,47 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
     while (pc < end && !g->err) {
         const WoRec* r = &g->prog[pc];
         if (r->op == WO_OP_BOUND) {
-            char c0[48], c1[48], c2[48], c3[48], c4[48];
-            flit(c0, r->f[0]);
-            flit(c1, r->f[1]);
-            flit(c2, r->f[2]);
-            flit(c3, r->f[3]);
-            flit(c4, r->f[4]);
+            static const char* nb[5] = {"bc0", "bc1", "bc2", "bc3", "bc4"};
+            uint32_t vb[5];
+            for (int i = 0; i < 5; ++i) vb[i] = fbits(r->f[i]);
             uint32_t k = g->nbound++;
-            bput(g->b, "%*sif (first) c%u = __ballot(wodev::bound_may_hit(%s, %s, %s, %s, %s, o, d)) != 0ull;\n",
-                 indent, "", k, c0, c1, c2, c3, c4);
-            bput(g->b, "%*sif (c%u) {\n", indent, "", k);
+            bput(g->b, "%*sif (first) {  // BOUND %u\n", indent, "", k);
+            emit_consts(g->b, indent + 2, "float", nb, vb, 5);
+            bput(g->b,
+                 "%*s  if (__ballot(wodev::bound_may_hit(bc0, bc1, bc2, bc3, bc4, o, d)) == 0ull) cull[%u] |= %uu;\n"
+                 "%*s}\n",
+                 indent, "", k / 32, 1u << (k % 32), indent, "");
+            bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
             gen_collect(g, pc + 1, r->u0, indent + 2);
             bput(g->b, "%*s}\n", indent, "");
             pc = r->u0;
         } else if (r->op == WO_OP_PRIM) {
             uint32_t ord = r->u1, cnt = r->u0;
+            static const char* nl[4] = {"c0", "c1", "c2", "c3"};
+            static const char* nk[2] = {"ka", "kb"};
             bput(g->b, "%*s{  // primitive %u (%u leaves)\n", indent, "", ord, cnt);
             bput(g->b, "%*s  wodev::Ivl iv; wodev::ivl_init(iv); float la, lb;\n", indent, "");
             for (uint32_t m = 0; m < cnt; ++m) {
                 const WoRec* L = &g->prog[pc + 1 + m];
-                char a[48], b[48], c[48], e[48];
-                flit(a, L->f[0]);
-                flit(b, L->f[1]);
-                flit(c, L->f[2]);
-                flit(e, L->f[3]);
-                bput(g->b, "%*s  wodev::%s_interval(%s, %s, %s, %s, o, d, la, lb); wodev::ivl_meet(iv, la, lb, %uu);\n",
-                     indent, "", L->op == WO_LEAF_SPHERE ? "sphere" : "halfspace", a, b, c, e, m);
+                uint32_t vl[4];
+                for (int i = 0; i < 4; ++i) vl[i] = fbits(L->f[i]);
+                bput(g->b, "%*s  {\n", indent, "");
+                emit_consts(g->b, indent + 4, "float", nl, vl, 4);
+                bput(g->b, "%*s    wodev::%s_interval(c0, c1, c2, c3, o, d, la, lb); wodev::ivl_meet(iv, la, lb, %uu);\n",
+                     indent, "", L->op == WO_LEAF_SPHERE ? "sphere" : "halfspace", m);
+                bput(g->b, "%*s  }\n", indent, "");
             }
+            uint32_t vk[2] = {ord << 12, (ord << 12) | (1u << 11)};
+            bput(g->b, "%*s  if (!(iv.a > iv.b)) {\n", indent, "");
+            emit_consts(g->b, indent + 4, "uint32_t", nk, vk, 2);
             bput(g->b,
-                 "%*s  if (!(iv.a > iv.b)) {\n"
                  "%*s    if (first) bits[%u] |= ((iv.a <= tmin && iv.b > tmin) ? 1u : 0u) << %u;\n"
-                 "%*s    if (iv.a > tmin) { uint64_t k = wodev::event_key(iv.a, %uu, 0u, iv.ma); if (k > after) "
+                 "%*s    if (iv.a > tmin) { uint64_t k = wodev::event_key_lo(iv.a, ka | iv.ma); if (k > after) "
                  "win.insert(k); }\n"
-                 "%*s    if (iv.b > tmin && iv.b < wodev::kInf) { uint64_t k = wodev::event_key(iv.b, %uu, 1u, iv.mb); "
+                 "%*s    if (iv.b > tmin && iv.b < wodev::kInf) { uint64_t k = wodev::event_key_lo(iv.b, kb | iv.mb); "
                  "if (k > after) win.insert(k); }\n"
                  "%*s  }\n%*s}\n",
-                 indent, "", indent, "", ord / 32, ord % 32, indent, "", ord, indent, "", ord, indent, "", indent,
-                 "");
+                 indent, "", ord / 32, ord % 32, indent, "", indent, "", indent, "", indent, "");
             pc += 1 + cnt;
         } else {
             ++pc; /* binops: nothing to collect */
@@ -138,7 +150,8 @@ static uint32_t gen_eval(Gen* g, uint32_t start, uint32_t end, int indent) {
         if (r->op == WO_OP_BOUND) {
             uint32_t k = g->nbound++;
             uint32_t v = g->nval++;
-            bput(g->b, "%*suint32_t v%u;\n%*sif (c%u) {\n", indent, "", v, indent, "", k);
+            bput(g->b, "%*suint32_t v%u;\n%*sif (!(cull[%u] & %uu)) {\n", indent, "", v, indent, "", k / 32,
+                 1u << (k % 32));
             uint32_t inner = gen_eval(g, pc + 1, r->u0, indent + 2);
             bput(g->b, "%*s  v%u = v%u;\n%*s} else {\n%*s  v%u = 0u;\n%*s}\n", indent, "", v, inner, indent, "",
                  indent, "", v, indent, "");
@@ -214,7 +227,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         bput(&b, "    const float tmin = WO_T_MIN;\n");
         bput(&b, "    uint32_t bits[%u];\n", nw);
         for (uint32_t w = 0; w < nw; ++w) bput(&b, "    bits[%u] = 0u;\n", w);
-        for (uint32_t k = 0; k < nbounds; ++k) bput(&b, "    bool c%u = true;\n", k);
+        uint32_t ncw = nbounds ? (nbounds + 31u) / 32u : 1u;
+        bput(&b, "    uint32_t cull[%u];  // bit k: BOUND k culled for this wave\n", ncw);
+        for (uint32_t w = 0; w < ncw; ++w) bput(&b, "    cull[%u] = 0u;\n", w);
         bput(&b,
              "    wodev::Window win; win.clear();\n"
              "    bool collect = true, first = true, have = false;\n"
@@ -255,7 +270,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "};\n");
     }
     bput(&b,
-         "\nextern \"C\" __global__ __launch_bounds__(256) void wo_jit_pathtrace(\n"
+         "\n#ifndef WO_JIT_MIN_WAVES\n#define WO_JIT_MIN_WAVES 4\n#endif\n"
+         "extern \"C\" __global__ __launch_bounds__(256, WO_JIT_MIN_WAVES) void wo_jit_pathtrace(\n"
          "    const WoRec* __restrict__ prog, const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t local_rows,\n"
          "    float4* __restrict__ out, unsigned long long* __restrict__ seg_out) {\n"
          "  JitTracer tr;\n"

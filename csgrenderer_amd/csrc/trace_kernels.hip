@@ -476,6 +476,25 @@ static std::unordered_map<uint64_t, std::vector<char>>& jit_cache() {
     return m;
 }
 
+// Extra hiprtc options from WOLOLO_JIT_FLAGS (space separated), e.g.
+// "-DWO_WINDOW=2 -DWO_JIT_MIN_WAVES=4" -- a tuning knob; part of the cache key.
+static std::vector<std::string> jit_extra_flags() {
+    std::vector<std::string> out;
+    const char* e = getenv("WOLOLO_JIT_FLAGS");
+    if (!e) return out;
+    std::string s(e), cur;
+    for (char c : s) {
+        if (c == ' ') {
+            if (!cur.empty()) out.push_back(cur);
+            cur.clear();
+        } else {
+            cur.push_back(c);
+        }
+    }
+    if (!cur.empty()) out.push_back(cur);
+    return out;
+}
+
 static int jit_compile(const char* src, const std::string& arch, std::vector<char>& code, char* err, size_t errlen) {
     hiprtcProgram p;
     const char* hdr_src[] = {kEmbed_wo_device_common_h, kEmbed_wo_scene_h};
@@ -485,8 +504,10 @@ static int jit_compile(const char* src, const std::string& arch, std::vector<cha
         return -1;
     }
     std::string arch_opt = "--offload-arch=" + arch;
-    const char* opts[] = {arch_opt.c_str(), "-O3", "-ffp-contract=off", "-std=c++17"};
-    hiprtcResult rc = hiprtcCompileProgram(p, 4, opts);
+    std::vector<std::string> extra = jit_extra_flags();
+    std::vector<const char*> opts = {arch_opt.c_str(), "-O3", "-ffp-contract=off", "-std=c++17"};
+    for (const std::string& f : extra) opts.push_back(f.c_str());
+    hiprtcResult rc = hiprtcCompileProgram(p, (int)opts.size(), opts.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t ls = 0;
         hiprtcGetProgramLogSize(p, &ls);
@@ -517,7 +538,9 @@ extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t err
         dev->jit_hash = 0;
         return 0;
     }
+    const char* flags = getenv("WOLOLO_JIT_FLAGS");
     uint64_t h = fnv1a(dev->arch.data(), dev->arch.size(), fnv1a(src, strlen(src)));
+    if (flags) h = fnv1a(flags, strlen(flags), h);
     if (dev->jit_fn && dev->jit_hash == h) return 0;
     std::vector<char> code;
     {

@@ -19,7 +19,7 @@ def test_csg32_source_compiles_for_gfx950(hostonly):
     nleaf = sum(1 for i in range(nrec) if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE))
     assert len(re.findall(r"wodev::(sphere|halfspace)_interval\(", src)) == nleaf
     nb = sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND)
-    assert len(re.findall(r"if \(first\) c\d+ = __ballot", src)) == nb
+    assert len(re.findall(r"if \(__ballot\(wodev::bound_may_hit\(", src)) == nb
     m = re.search(r"kOrdPc\[(\d+)\] = \{([^}]*)\}", src)
     assert int(m.group(1)) == nprim
     pcs = [int(x.strip().rstrip("u")) for x in m.group(2).split(",")]
@@ -30,19 +30,19 @@ def test_csg32_source_compiles_for_gfx950(hostonly):
 
 
 def test_literals_round_trip(hostonly):
-    """Leaf parameters are emitted as hex-float literals that round-trip exactly."""
+    """Leaf parameters are emitted as exact fp32 bit patterns (s_mov_b32 immediates)."""
     r = wl.Renderer("lit", max_nodes=8)
     s = r.sphere(0.1)
     h = r.halfspace((0.3, -0.7, 0.2))
     r.union(wl.arg(s, (1.0 / 3.0, 2.0 / 7.0, -1e-7)), wl.arg(h, (0.1, 0.2, 0.3)))
     prog, nrec, _ = r.program()
     src = r.jit_source()
-    lits = [float.fromhex(x) for x in re.findall(r"(-?0x[0-9a-f.]+p[-+]\d+)f", src)]
+    imms = {int(x, 16) for x in re.findall(r"s_mov_b32 %\d, 0x([0-9a-f]{8})", src)}
     for i in range(nrec):
         if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE):
             for k in range(4):
-                v = prog[i].f[k]
-                assert any(np.float32(x) == np.float32(v) for x in lits), v
+                bits = int(np.array(prog[i].f[k], dtype=np.float32).view(np.uint32))
+                assert bits in imms, prog[i].f[k]
     assert wl.jit_compile_check(src) == ""
     r.close()
 
