@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--jit", type=int, default=1, help="1: scene-specialised kernel (auto), 0: interpreter kernel")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo stages the gather through host memory (for rehearsing N>1 ranks on one GPU)")
+    ap.add_argument("--verify", action="store_true",
+                    help="rank 0 checks the assembled frame against a single full-frame render (bit-exact)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-dispatch HBM bytes measured by rocprofv3 --pmc (profiles/*.json) for roofline.traffic")
     return ap.parse_args()
@@ -61,10 +65,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    dev_index = local_rank % max(ndev, 1)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    gloo = args.dist_backend == "gloo"
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from csgrenderer_amd import scenes
     from csgrenderer_amd import wololo as wl
@@ -87,9 +97,11 @@ def main():
     lr = wl.local_rows(H, T, world)
     out = torch.empty((lr, W, 4), dtype=torch.float32, device=dev)
     seg = torch.zeros(1, dtype=torch.int64, device=dev)
-    gathered = frame = None
+    stacked = gathered = frame = None
     if world > 1 and rank == 0:
-        gathered = [torch.empty((lr, W, 4), dtype=torch.float32, device=dev) for _ in range(world)]
+        # one rank-major buffer; the gather writes each rank's tiles into its slice
+        stacked = torch.empty((world, lr, W, 4), dtype=torch.float32, device="cpu" if gloo else dev)
+        gathered = list(stacked.unbind(0))
         frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
@@ -103,12 +115,13 @@ def main():
         if i is not None:
             k_end[i].record(stream)
         if world > 1:
+            src = out.cpu() if gloo else out
             if rank == 0:
-                dist.gather(out, gather_list=gathered, dst=0)
-                stacked = torch.stack(gathered)  # rank-major [N, lr, W, 4]
-                wl.assemble_rows_device(stacked.data_ptr(), frame.data_ptr(), W, H, T, world, sh)
+                dist.gather(src, gather_list=gathered, dst=0)
+                g = stacked.to(dev, non_blocking=False) if gloo else stacked
+                wl.assemble_rows_device(g.data_ptr(), frame.data_ptr(), W, H, T, world, sh)
             else:
-                dist.gather(out, dst=0)
+                dist.gather(src, dst=0)
 
     for _ in range(args.warmup):
         step()
@@ -124,8 +137,9 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    segs_total = seg.clone()
+    coll = "cpu" if gloo else dev  # gloo reduces host tensors
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=coll)
+    segs_total = seg.clone().to(coll)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
         dist.all_reduce(segs_total, op=dist.ReduceOp.SUM)
@@ -133,6 +147,23 @@ def main():
     segs_local = int(seg.item())
     segs_all = int(segs_total.item())
     k_ms = sum(k_start[i].elapsed_time(k_end[i]) for i in range(args.steps)) / args.steps
+
+    verified = None
+    if args.verify and rank == 0:
+        import numpy as np
+        full = r.render(params)
+        got = (frame if world > 1 else out[:H]).cpu().numpy()
+        verified = bool(np.array_equal(got, full))
+        if not verified:
+            bad = int((got != full).any(axis=-1).sum())
+            print(f"[bench] VERIFY FAILED: {bad} pixels of the assembled frame differ from a full render",
+                  file=sys.stderr)
+    if world > 1:
+        flag = torch.tensor([0 if verified is False else 1], dtype=torch.int32, device="cpu" if gloo else dev)
+        dist.broadcast(flag, src=0)
+        verified_all = bool(flag.item())
+    else:
+        verified_all = verified is not False
 
     if rank == 0:
         steps = args.steps
@@ -144,7 +175,8 @@ def main():
             achieved_tf = flop_launch / (k_ms * 1e-3) / 1e12
             roof = {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4), "traffic": None,
-                    "kernel": "pathtrace_kernel", "kernel_ms": round(k_ms, 4),
+                    "kernel": "wo_jit_pathtrace" if r.trace_path() == "jit" else "pathtrace_kernel",
+                    "kernel_ms": round(k_ms, 4),
                     "flop_per_segment": info.flop_per_segment,
                     "segments_per_launch": segs_local // steps, "trace_path": r.trace_path()}
         else:
@@ -175,7 +207,7 @@ def main():
                                    f"{info.spheres} spheres + {info.halfspaces} half-spaces, {info.binops} binops",
                        "scene": info.name, "width": W, "height": H, "spp": params.spp,
                        "max_depth": params.max_depth, "tile_rows": T,
-                       "parallelism": f"row-cyclic tiles x{world}" + (" + RCCL gather" if world > 1 else "")},
+                       "parallelism": f"row-cyclic tiles x{world}" + (f" + {'gloo (host-staged)' if gloo else 'RCCL'} gather" if world > 1 else "")},
             "fps": round(steps / elapsed_s, 3),
             "msamples_per_s": round(samples * steps / elapsed_s / 1e6, 3),
             "segments_per_frame": segs_all // steps,
@@ -184,10 +216,14 @@ def main():
                                    "unit": "GB/s", "frac": round(hbm_gbs / PEAK_HBM_GBS, 6)},
             "cpu_baseline": cpu,
         }
+        if verified is not None:
+            line["verified_vs_full_render"] = verified
         print(json.dumps(line), flush=True)
     r.close()
     if world > 1:
         dist.destroy_process_group()
+    if not verified_all:
+        sys.exit(3)
 
 
 def cpu_baseline(r, params, budget_s: float):
