@@ -17,7 +17,7 @@
  *   3. operands are emitted larger-stack-need first (Sethi-Ullman), so the
  *      kernel's 32-bit evaluation stack never overflows; DIFF becomes RDIFF
  *      when the subtrahend is emitted first;
- *   4. subtrees with >= 3 leaves and a finite extent get a conservative
+ *   4. subtrees with >= 2 leaves (WOLOLO_BOUND_MIN_LEAVES) and a finite extent get a conservative
  *      WO_OP_BOUND sphere so a wave whose rays all miss can skip them.
  */
 #include <math.h>
@@ -58,6 +58,7 @@ typedef struct Ctx {
     char* err;
     size_t errlen;
     int failed;
+    int bound_min_leaves; /* smallest subtree (in leaves) that gets a BOUND record */
 } Ctx;
 
 #define MAX_EXPANDED_NODES (1u << 21)
@@ -455,7 +456,7 @@ static void emit_leaf(Ctx* c, const ENode* m) {
 static void emit(Ctx* c, int id, double outer_r) {
     if (c->failed) return;
     ENode* e = &c->e[id];
-    int use_bound = e->bounded && e->leaves >= 3 && e->br < 0.7 * outer_r;
+    int use_bound = e->bounded && e->leaves >= c->bound_min_leaves && e->br < 0.7 * outer_r;
     double inner_r = use_bound ? e->br : outer_r;
     uint32_t bidx = 0;
     if (use_bound) {
@@ -519,6 +520,11 @@ int wo_compile_scene(Wo_Renderer* r, char* err, size_t errlen) {
     c.r = r;
     c.err = err;
     c.errlen = errlen;
+    c.bound_min_leaves = 2;
+    {
+        const char* v = getenv("WOLOLO_BOUND_MIN_LEAVES");
+        if (v && *v) c.bound_min_leaves = atoi(v) > 1 ? atoi(v) : 2;
+    }
 
     int* roots = (int*)malloc(sizeof(int) * (r->node_count ? r->node_count : 1));
     if (!roots) {
