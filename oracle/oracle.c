@@ -132,17 +132,45 @@ static void normalize3(float v[3]) {
     v[2] = v[2] * inv;
 }
 
-static void rand_in_unit_sphere(uint32_t* rng, float p[3]) {
-    for (int i = 0; i < 64; ++i) {
-        p[0] = 2.0f * rng_float(rng) - 1.0f;
-        p[1] = 2.0f * rng_float(rng) - 1.0f;
-        p[2] = 2.0f * rng_float(rng) - 1.0f;
-        float l2 = dot3(p, p);
-        if (l2 < 1.0f && l2 > 1e-12f) return;
+/* sin and cos of the angle 2*pi*u: reduce to the nearest quarter turn, then
+ * fp32 minimax polynomials (Cephes sinf/cosf coefficients) on [-pi/4, pi/4],
+ * one rounding per written operation. */
+static void sincos_turn(float u, float* s, float* c) {
+    float quarter_turns = u * 4.0f;
+    float q = rintf(quarter_turns); /* round half to even, as v_rndne_f32 */
+    float x = (quarter_turns - q) * 1.57079637f;
+    float xx = x * x;
+    float ps = -1.9515295891e-4f * xx;
+    ps = ps + 8.3321608736e-3f;
+    ps = ps * xx;
+    ps = ps - 1.6666654611e-1f;
+    ps = ps * xx;
+    ps = ps * x;
+    float sin_x = x + ps;
+    float pc = 2.443315711809948e-5f * xx;
+    pc = pc - 1.388731625493765e-3f;
+    pc = pc * xx;
+    pc = pc + 4.166664568298827e-2f;
+    pc = pc * xx;
+    pc = pc * xx;
+    float cos_x = (1.0f - 0.5f * xx) + pc;
+    switch ((unsigned)(int)q & 3u) {
+    case 0: *s = sin_x; *c = cos_x; break;
+    case 1: *s = cos_x; *c = -sin_x; break;
+    case 2: *s = -sin_x; *c = -cos_x; break;
+    default: *s = -cos_x; *c = sin_x; break;
     }
-    p[0] = 0.0f;
-    p[1] = 0.0f;
-    p[2] = 1.0f;
+}
+
+/* Uniform unit vector: z uniform in [-1, 1], azimuth uniform. */
+static void rand_unit_vector(uint32_t* rng, float p[3]) {
+    float z = 1.0f - 2.0f * rng_float(rng);
+    float r = sqrtf(1.0f - z * z);
+    float s, c;
+    sincos_turn(rng_float(rng), &s, &c);
+    p[0] = r * c;
+    p[1] = r * s;
+    p[2] = z;
 }
 
 /* Ray interval of one leaf; empty = [+inf, -inf]. */
@@ -398,12 +426,11 @@ static void shade_pixel(const WoRec* prog, uint32_t n, const WoMaterial* mats, u
         }
         float off[3] = {0.0f, 0.0f, 0.0f};
         if (cam->lens_radius > 0.0f && !normals) {
-            float px = 0.0f, py = 0.0f;
-            for (int i = 0; i < 64; ++i) {
-                px = 2.0f * rng_float(&rng) - 1.0f;
-                py = 2.0f * rng_float(&rng) - 1.0f;
-                if (px * px + py * py < 1.0f) break;
-            }
+            /* point on the unit disk: radius sqrt(u), angle 2*pi*v */
+            float rad = sqrtf(rng_float(&rng));
+            float s, c;
+            sincos_turn(rng_float(&rng), &s, &c);
+            float px = rad * c, py = rad * s;
             float rx = cam->lens_radius * px, ry = cam->lens_radius * py;
             for (int i = 0; i < 3; ++i) off[i] = cam->u[i] * rx + cam->v[i] * ry;
         }
@@ -449,8 +476,7 @@ static void shade_pixel(const WoRec* prog, uint32_t n, const WoMaterial* mats, u
             float nd[3], att[3];
             if (m->kind == WO_MAT_LAMBERTIAN) {
                 float ru[3];
-                rand_in_unit_sphere(&rng, ru);
-                normalize3(ru);
+                rand_unit_vector(&rng, ru);
                 float sd[3] = {N[0] + ru[0], N[1] + ru[1], N[2] + ru[2]};
                 if (fabsf(sd[0]) < 1e-8f && fabsf(sd[1]) < 1e-8f && fabsf(sd[2]) < 1e-8f) {
                     sd[0] = N[0];
@@ -463,7 +489,7 @@ static void shade_pixel(const WoRec* prog, uint32_t n, const WoMaterial* mats, u
             } else if (m->kind == WO_MAT_METAL) {
                 float k = 2.0f * dot3(d, N);
                 float rs[3];
-                rand_in_unit_sphere(&rng, rs);
+                rand_unit_vector(&rng, rs); /* RTIOW v4 fuzz: unit vector */
                 float sc[3];
                 for (int i = 0; i < 3; ++i) sc[i] = (d[i] - k * N[i]) + m->fuzz * rs[i];
                 if (!(dot3(sc, N) > 0.0f)) break; /* absorbed */
@@ -569,3 +595,5 @@ int oracle_pathtrace_rows(WoRec const* prog, uint32_t n_recs, WoMaterial const* 
     if (segments) *segments = total;
     return fail ? -1 : 0;
 }
+
+void oracle_sincos_turn(float u, float* s, float* c) { sincos_turn(u, s, c); }

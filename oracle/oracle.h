@@ -46,6 +46,9 @@ int oracle_pathtrace_rows(WoRec const* prog, uint32_t n_recs, WoMaterial const* 
 int oracle_trace(WoRec const* prog, uint32_t n_recs, float const o[3], float const d[3], float* t, uint32_t* prim,
                  uint32_t* type, uint32_t* member, uint32_t* root_after);
 
+/* sin/cos of 2*pi*u as the kernels compute it (polynomial, no libm). */
+void oracle_sincos_turn(float u, float* s, float* c);
+
 /* RNG known answers. */
 uint32_t oracle_pcg_hash(uint32_t v);
 uint32_t oracle_rng_next(uint32_t* state);

@@ -112,3 +112,20 @@ def test_rng_uniform_in_unit_interval():
     vals = [(lib.oracle_rng_next(ctypes.byref(st)) >> 8) * 2.0 ** -24 for _ in range(20000)]
     assert 0.0 <= min(vals) and max(vals) < 1.0
     assert abs(np.mean(vals) - 0.5) < 0.01
+
+
+def test_sincos_turn_accuracy():
+    """The polynomial sin/cos of 2*pi*u used for direction sampling (both kernels and
+    oracle): within a few fp32 ulps of float64 sin/cos over [0, 1)."""
+    import ctypes
+    lib = pyoracle.load()
+    lib.oracle_sincos_turn.argtypes = [ctypes.c_float, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    s, c = ctypes.c_float(), ctypes.c_float()
+    us = np.concatenate([np.linspace(0, 1, 4001, endpoint=False), np.random.default_rng(0).random(4000)])
+    err = 0.0
+    for u in us.astype(np.float32):
+        lib.oracle_sincos_turn(float(u), ctypes.byref(s), ctypes.byref(c))
+        a = 2 * np.pi * float(u)
+        err = max(err, abs(s.value - np.sin(a)), abs(c.value - np.cos(a)))
+        assert abs(s.value * s.value + c.value * c.value - 1.0) < 1e-6
+    assert err < 4e-7, err
