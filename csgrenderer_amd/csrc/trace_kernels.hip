@@ -41,7 +41,8 @@ namespace {
 using namespace wodev;
 
 // 4-bit op codes of the per-wave compacted program (8 per dword).
-constexpr uint32_t kCodePrim = 1, kCodeUnion = 2, kCodeInter = 3, kCodeDiff = 4, kCodeConst0 = 6;
+// (2..5 are WO_OP_UNION, _INTER, _DIFF, _RDIFF unchanged)
+constexpr uint32_t kCodePrim = 1, kCodeUnion = 2, kCodeConst0 = 6;
 
 // Per-wave LDS scratch layout (dwords), computed on the host.
 struct KLayout {
@@ -95,33 +96,28 @@ struct InterpTracer {
             hib[w * 64u + lane] ^= 1u << ((ord - 64u) & 31u);
         }
     }
-    // Root value over the compacted program, 32-deep bit stack.
+    // Root value over the compacted program, 32-deep bit stack, branch-free per
+    // node: value = bit idx of the code's truth table, idx = 2A+B for binops (A
+    // second, B top of stack) or the primitive's membership bit; binops pop two.
+    //   PRIM 0b0010, UNION 0b1110, INTER 0b1000, DIFF 0b0100, RDIFF 0b0010, CONST0 0.
+    static constexpr uint32_t kTruth =
+        (0x2u << 4) | (0xEu << 8) | (0x8u << 12) | (0x4u << 16) | (0x2u << 20) | (0x0u << 24);
     __device__ __forceinline__ uint32_t eval_root() const {
         uint32_t st = 0, ord = 0;
-        uint32_t nwords = (ncodes + 7u) >> 3;
-        for (uint32_t w = 0; w < nwords; ++w) {
-            uint32_t word = uni(codes[w]);
-            uint32_t n = ncodes - w * 8u;
-            n = n < 8u ? n : 8u;
-            for (uint32_t j = 0; j < n; ++j) {
+        const uint32_t n = ncodes;
+        for (uint32_t base = 0; base < n; base += 8u) {
+            uint32_t word = uni(codes[base >> 3]);
+            uint32_t m = n - base < 8u ? n - base : 8u;
+            for (uint32_t j = 0; j < m; ++j) {
                 uint32_t c = (word >> (4u * j)) & 15u;
-                if (c == kCodePrim) {
-                    st = (st << 1) | bit(ord);
-                    ++ord;
-                } else if (c == kCodeConst0) {
-                    st = st << 1;
-                } else {
-                    uint32_t r;
-                    if (c == kCodeUnion)
-                        r = (st | (st >> 1)) & 1u;
-                    else if (c == kCodeInter)
-                        r = (st & (st >> 1)) & 1u;
-                    else if (c == kCodeDiff)
-                        r = (st >> 1) & ~st & 1u;
-                    else
-                        r = st & ~(st >> 1) & 1u;
-                    st = ((st >> 1) & ~1u) | r;
-                }
+                uint32_t tt = (kTruth >> (4u * c)) & 15u;
+                bool isprim = c == kCodePrim;
+                uint32_t pop = (c >= kCodeUnion && c < kCodeConst0) ? 2u : 0u;
+                uint32_t idx = st & 3u;
+                if (isprim) idx = bit(ord);
+                uint32_t val = (tt >> idx) & 1u;
+                st = ((st >> pop) << 1) | val;
+                ord += isprim ? 1u : 0u;
             }
         }
         return st & 1u;
@@ -139,6 +135,7 @@ struct InterpTracer {
         nprims = 0;
         uint32_t code_acc = 0;
         uint32_t hib_acc = 0;
+        uint32_t st = 0;  // bit stack: the root value at t_min, evaluated on the way
 
         // pass 1: walk the program, cull, intersect, collect events
         uint32_t pc = 0;
@@ -153,6 +150,7 @@ struct InterpTracer {
                     continue;
                 }
                 code = kCodeConst0;
+                st = st << 1;
                 pc = uni(rec.u0);
             } else if (op == WO_OP_PRIM) {
                 uint32_t count = uni(rec.u0);
@@ -177,9 +175,12 @@ struct InterpTracer {
                 ordpc[ord] = pc;
                 nprims = ord + 1u;
                 code = kCodePrim;
+                st = (st << 1) | inside;
                 pc += 1u + count;
             } else {
                 code = op;  // WO_OP_UNION..RDIFF share values with the codes
+                uint32_t tt = (kTruth >> (4u * code)) & 15u;
+                st = ((st >> 2) << 1) | ((tt >> (st & 3u)) & 1u);
                 ++pc;
             }
             uint32_t slot = ncodes & 7u;
@@ -195,7 +196,7 @@ struct InterpTracer {
 
         // pass 2: sweep events in key order; the first root flip is the hit
         if (win.k[0] == kEmptyKey) return false;
-        uint32_t root = eval_root();
+        uint32_t root = st & 1u;
         while (win.k[0] != kEmptyKey) {
             uint64_t key = win.pop();
             uint32_t ord = ((uint32_t)key) >> 12;
