@@ -448,6 +448,11 @@ static void emit_leaf(Ctx* c, const ENode* m) {
         rec->f[1] = (float)m->n[1];
         rec->f[2] = (float)m->n[2];
         rec->f[3] = (float)m->h;
+        /* axis-aligned normal (exactly, in fp32): flag the axis (wo_scene.h) */
+        for (int a = 0; a < 3; ++a) {
+            int b = (a + 1) % 3, c = (a + 2) % 3;
+            if ((rec->f[a] == 1.0f || rec->f[a] == -1.0f) && rec->f[b] == 0.0f && rec->f[c] == 0.0f) rec->u1 = 1u + a;
+        }
     }
 }
 

@@ -117,9 +117,22 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
                 uint32_t vl[4];
                 for (int i = 0; i < 4; ++i) vl[i] = fbits(L->f[i]);
                 bput(g->b, "%*s  {\n", indent, "");
-                emit_consts(g->b, indent + 4, "float", nl, vl, 4);
-                bput(g->b, "%*s    wodev::%s_interval(c0, c1, c2, c3, o, d, la, lb); wodev::ivl_meet(iv, la, lb, %uu);\n",
-                     indent, "", L->op == WO_LEAF_SPHERE ? "sphere" : "halfspace", m);
+                if (L->op == WO_LEAF_HALFSPACE && L->u1 != 0u) {
+                    /* axis-aligned: s = +-1 stays a literal (inline constant), h in an SGPR */
+                    static const char* nh[1] = {"c3"};
+                    static const char axis[3] = {'x', 'y', 'z'};
+                    char ax = axis[L->u1 - 1u];
+                    emit_consts(g->b, indent + 4, "float", nh, &vl[3], 1);
+                    bput(g->b,
+                         "%*s    wodev::halfspace_axis_interval(%s, c3, o.%c, d.%c, iv%c, la, lb); "
+                         "wodev::ivl_meet(iv, la, lb, %uu);\n",
+                         indent, "", L->f[L->u1 - 1u] > 0.0f ? "1.0f" : "-1.0f", ax, ax, ax, m);
+                } else {
+                    emit_consts(g->b, indent + 4, "float", nl, vl, 4);
+                    bput(g->b,
+                         "%*s    wodev::%s_interval(c0, c1, c2, c3, o, d, la, lb); wodev::ivl_meet(iv, la, lb, %uu);\n",
+                         indent, "", L->op == WO_LEAF_SPHERE ? "sphere" : "halfspace", m);
+                }
                 bput(g->b, "%*s  }\n", indent, "");
             }
             uint32_t vk[2] = {ord << 12, (ord << 12) | (1u << 11)};
@@ -225,6 +238,12 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         bput(&b, "    return false;\n  }\n};\n");
     } else {
         bput(&b, "    const float tmin = WO_T_MIN;\n");
+        /* reciprocal direction components for the axes axis-aligned half-spaces use */
+        uint32_t axes = 0;
+        for (uint32_t i = 0; i < n_recs; ++i)
+            if (prog[i].op == WO_LEAF_HALFSPACE && prog[i].u1 >= 1u && prog[i].u1 <= 3u) axes |= 1u << (prog[i].u1 - 1u);
+        for (int a = 0; a < 3; ++a)
+            if (axes & (1u << a)) bput(&b, "    const float iv%c = 1.0f / d.%c;\n", "xyz"[a], "xyz"[a]);
         bput(&b, "    uint32_t bits[%u];\n", nw);
         for (uint32_t w = 0; w < nw; ++w) bput(&b, "    bits[%u] = 0u;\n", w);
         uint32_t ncw = nbounds ? (nbounds + 31u) / 32u : 1u;

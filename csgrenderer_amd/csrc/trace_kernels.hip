@@ -57,15 +57,22 @@ struct ProgPtr {
     __device__ __forceinline__ WoRec operator[](uint32_t i) const { return p[i]; }
 };
 
+// `inv`/`have_inv`: the ray's reciprocal direction, computed on the first
+// axis-aligned half-space met (wave-uniform condition).
 template <class Prog>
-__device__ __forceinline__ Ivl prim_interval(Prog prog, uint32_t pc, uint32_t count, F3 o, F3 d) {
+__device__ __forceinline__ Ivl prim_interval(Prog prog, uint32_t pc, uint32_t count, F3 o, F3 d, F3& inv,
+                                             bool& have_inv) {
     Ivl iv;
     ivl_init(iv);
     for (uint32_t m = 0; m < count; ++m) {
         WoRec L = prog[pc + 1u + m];
         uint32_t kind = uni(L.op);
+        if (kind == WO_LEAF_HALFSPACE && !have_inv && uni(L.u1) != 0u) {
+            inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+            have_inv = true;
+        }
         float la, lb;
-        leaf_interval(L, kind, o, d, la, lb);
+        leaf_interval(L, kind, o, d, inv, la, lb);
         ivl_meet(iv, la, lb, m);
     }
     return iv;
@@ -136,6 +143,8 @@ struct InterpTracer {
         uint32_t code_acc = 0;
         uint32_t hib_acc = 0;
         uint32_t st = 0;  // bit stack: the root value at t_min, evaluated on the way
+        F3 inv = f3(0.0f, 0.0f, 0.0f);
+        bool have_inv = false;
 
         // pass 1: walk the program, cull, intersect, collect events
         uint32_t pc = 0;
@@ -155,7 +164,7 @@ struct InterpTracer {
             } else if (op == WO_OP_PRIM) {
                 uint32_t count = uni(rec.u0);
                 uint32_t ord = nprims;
-                Ivl iv = prim_interval(prog, pc, count, o, d);
+                Ivl iv = prim_interval(prog, pc, count, o, d, inv, have_inv);
                 uint32_t inside = 0;
                 if (!(iv.a > iv.b)) {
                     inside = (iv.a <= tmin && iv.b > tmin) ? 1u : 0u;
@@ -221,7 +230,7 @@ struct InterpTracer {
                         if (((word >> (4u * j)) & 15u) != kCodePrim) continue;
                         uint32_t ppc = uni(ordpc[ordc]);
                         uint32_t count = uni(prog[ppc].u0);
-                        Ivl iv = prim_interval(prog, ppc, count, o, d);
+                        Ivl iv = prim_interval(prog, ppc, count, o, d, inv, have_inv);
                         if (!(iv.a > iv.b)) {
                             if (iv.a > tmin) {
                                 uint64_t k2 = event_key(iv.a, ordc, 0u, iv.ma);

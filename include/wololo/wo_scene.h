@@ -48,7 +48,11 @@ enum {
 
 enum {
     WO_LEAF_SPHERE = 16,     /* f: cx cy cz r^2 1/r */
-    WO_LEAF_HALFSPACE = 17,  /* f: nx ny nz h   ({x : n.x <= h}, |n| = 1) */
+    WO_LEAF_HALFSPACE = 17,  /* f: nx ny nz h   ({x : n.x <= h}, |n| = 1);
+                              * u1 = 1 + a when n is exactly s*e_a (s = +-1, a = 0,1,2
+                              * for x,y,z), else 0.  Such a half-space is intersected
+                              * as t = (h - s*o_a) * (s * (1/d_a)), the reciprocal taken
+                              * once per ray, instead of (h - n.o) / (n.d). */
 };
 
 typedef struct WoRec {

@@ -193,8 +193,23 @@ static void leaf_span(const WoRec* L, const float o[3], const float d[3], float*
     }
     /* half-space {x : n.x <= h} */
     float n[3] = {L->f[0], L->f[1], L->f[2]};
-    float den = dot3(n, d);
-    float dist = L->f[3] - dot3(n, o);
+    float den, dist;
+    if (L->u1 != 0u) {
+        /* axis-aligned n = s*e_a (wo_scene.h): t = (h - s*o_a) * (s*(1/d_a)) */
+        uint32_t a = L->u1 - 1u;
+        float s = n[a];
+        den = s * d[a];
+        dist = L->f[3] - s * o[a];
+        if (den != 0.0f) {
+            float t = dist * (s * (1.0f / d[a]));
+            *lo = den > 0.0f ? -INFINITY : t;
+            *hi = den > 0.0f ? t : INFINITY;
+            return;
+        }
+    } else {
+        den = dot3(n, d);
+        dist = L->f[3] - dot3(n, o);
+    }
     if (den == 0.0f) {
         if (dist >= 0.0f) {
             *lo = -INFINITY;

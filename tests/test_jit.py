@@ -17,7 +17,11 @@ def test_csg32_source_compiles_for_gfx950(hostonly):
     assert src is not None
     # one intersection call per leaf, one cull flag per BOUND, ordinal table of every primitive
     nleaf = sum(1 for i in range(nrec) if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE))
-    assert len(re.findall(r"wodev::(sphere|halfspace)_interval\(", src)) == nleaf
+    assert len(re.findall(r"wodev::(sphere|halfspace|halfspace_axis)_interval\(", src)) == nleaf
+    # the slab and the cube are axis-aligned: tagged by the compiler, emitted on the fast path
+    naxis = sum(1 for i in range(nrec) if prog[i].op == wl.WO_LEAF_HALFSPACE and prog[i].u1 != 0)
+    assert naxis >= 12
+    assert len(re.findall(r"wodev::halfspace_axis_interval\(", src)) == naxis
     nb = sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND)
     assert len(re.findall(r"if \(__ballot\(wodev::bound_may_hit\(", src)) == nb
     m = re.search(r"kOrdPc\[(\d+)\] = \{([^}]*)\}", src)
@@ -40,7 +44,9 @@ def test_literals_round_trip(hostonly):
     imms = {int(x, 16) for x in re.findall(r"s_mov_b32 %\d, 0x([0-9a-f]{8})", src)}
     for i in range(nrec):
         if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE):
-            for k in range(4):
+            # axis-aligned half-spaces carry only h as an SGPR constant (s is a literal)
+            ks = [3] if prog[i].op == wl.WO_LEAF_HALFSPACE and prog[i].u1 else range(4)
+            for k in ks:
                 bits = int(np.array(prog[i].f[k], dtype=np.float32).view(np.uint32))
                 assert bits in imms, prog[i].f[k]
     assert wl.jit_compile_check(src) == ""

@@ -76,7 +76,9 @@ def _rand_quat(rng):
     return wl.Quaternion(v[0], wl.Vec3(v[1], v[2], v[3]))
 
 
-def _random_scene(seed, n_leaves=10):
+def _random_scene(seed, n_leaves=10, axis=False):
+    """axis=True: half-space normals are +-e_a and operands are only translated, so
+    the compiled leaves are axis-aligned (u1 != 0) and take the reciprocal path."""
     rng = np.random.default_rng(seed)
     r = wl.Renderer(f"rand{seed}", max_nodes=256)
     sh = Shadow(r)
@@ -85,13 +87,14 @@ def _random_scene(seed, n_leaves=10):
         if rng.random() < 0.7:
             pool.append(sh.sphere(rng.uniform(0.4, 1.2)))
         else:
-            pool.append(sh.halfspace(rng.normal(size=3)))
+            nrm = np.eye(3)[rng.integers(3)] * rng.choice([-1.0, 1.0]) if axis else rng.normal(size=3)
+            pool.append(sh.halfspace(nrm))
     while len(pool) > 1:
         i, j = rng.choice(len(pool), 2, replace=False)
         a, b = pool[i], pool[j]
         op = rng.choice(["u", "i", "d"], p=[0.45, 0.3, 0.25])
         mk = lambda n: wl.arg(n, tuple(rng.uniform(-1.0, 1.0, 3)),
-                              _rand_quat(rng) if rng.random() < 0.5 else None)
+                              _rand_quat(rng) if rng.random() < 0.5 and not axis else None)
         n = sh.binop(op, mk(a), mk(b))
         pool = [x for k, x in enumerate(pool) if k not in (i, j)] + [n]
     return r, sh, rng
@@ -105,7 +108,14 @@ def _program_checks(prog, nrec, nprim):
         if op == wl.WO_OP_PRIM:
             ords.append(prog[pc].u1)
             for m in range(prog[pc].u0):
-                assert prog[pc + 1 + m].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE)
+                L = prog[pc + 1 + m]
+                assert L.op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE)
+                if L.op == wl.WO_LEAF_HALFSPACE:
+                    # u1 = 1 + a exactly when the normal is +-e_a (wo_scene.h)
+                    f = list(L.f[:3])
+                    axes = [a for a in range(3) if abs(f[a]) == 1.0 and f[(a + 1) % 3] == 0.0
+                            and f[(a + 2) % 3] == 0.0]
+                    assert L.u1 == (1 + axes[0] if axes else 0), (f, L.u1)
             sp += 1
             pc += 1 + prog[pc].u0
         elif op == wl.WO_OP_BOUND:
@@ -178,11 +188,13 @@ def test_bounds_enclose_their_spheres(hostonly):
     assert checked > 480
 
 
-@pytest.mark.parametrize("seed", range(12))
-def test_random_scenes_hits_match_float64_classifier(hostonly, seed):
-    r, sh, rng = _random_scene(seed)
+@pytest.mark.parametrize("seed,axis", [(s, False) for s in range(12)] + [(s, True) for s in range(100, 106)])
+def test_random_scenes_hits_match_float64_classifier(hostonly, seed, axis):
+    r, sh, rng = _random_scene(seed, axis=axis)
     prog, nrec, nprim = r.program()
     _program_checks(prog, nrec, nprim)
+    if axis:
+        assert all(prog[i].u1 != 0 for i in range(nrec) if prog[i].op == wl.WO_LEAF_HALFSPACE)
     n_hit = n_checked = 0
     for _ in range(60):
         o = rng.uniform(-4, 4, 3) * np.array([1, 1, 1]) + np.array([0, 0, 6.0])
