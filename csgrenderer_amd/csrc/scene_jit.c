@@ -111,7 +111,7 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
             static const char* nl[4] = {"c0", "c1", "c2", "c3"};
             static const char* nk[2] = {"ka", "kb"};
             bput(g->b, "%*s{  // primitive %u (%u leaves)\n", indent, "", ord, cnt);
-            bput(g->b, "%*s  wodev::Ivl iv; wodev::ivl_init(iv); float la, lb;\n", indent, "");
+            bput(g->b, "%*s  wodev::Ivl iv; float la, lb;\n", indent, "");
             for (uint32_t m = 0; m < cnt; ++m) {
                 const WoRec* L = &g->prog[pc + 1 + m];
                 uint32_t vl[4];
@@ -124,28 +124,31 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
                     char ax = axis[L->u1 - 1u];
                     emit_consts(g->b, indent + 4, "float", nh, &vl[3], 1);
                     bput(g->b,
-                         "%*s    wodev::halfspace_axis_interval(%s, c3, o.%c, d.%c, iv%c, la, lb); "
-                         "wodev::ivl_meet(iv, la, lb, %uu);\n",
-                         indent, "", L->f[L->u1 - 1u] > 0.0f ? "1.0f" : "-1.0f", ax, ax, ax, m);
+                         "%*s    wodev::halfspace_axis_interval(%s, c3, o.%c, d.%c, iv%c, la, lb);\n",
+                         indent, "", L->f[L->u1 - 1u] > 0.0f ? "1.0f" : "-1.0f", ax, ax, ax);
                 } else {
                     emit_consts(g->b, indent + 4, "float", nl, vl, 4);
                     bput(g->b,
-                         "%*s    wodev::%s_interval(c0, c1, c2, c3, o, d, la, lb); wodev::ivl_meet(iv, la, lb, %uu);\n",
-                         indent, "", L->op == WO_LEAF_SPHERE ? "sphere" : "halfspace", m);
+                         "%*s    wodev::%s_interval(c0, c1, c2, c3, o, d, la, lb);\n",
+                         indent, "", L->op == WO_LEAF_SPHERE ? "sphere" : "halfspace");
                 }
+                if (m == 0)
+                    bput(g->b, "%*s    wodev::ivl_first(iv, la, lb);\n", indent, "");
+                else
+                    bput(g->b, "%*s    wodev::ivl_meet(iv, la, lb, %uu);\n", indent, "", m);
                 bput(g->b, "%*s  }\n", indent, "");
             }
             uint32_t vk[2] = {ord << 12, (ord << 12) | (1u << 11)};
             bput(g->b, "%*s  if (!(iv.a > iv.b)) {\n", indent, "");
             emit_consts(g->b, indent + 4, "uint32_t", nk, vk, 2);
+            /* one lane branch per event: the key test against `after` (re-collect) folded in */
             bput(g->b,
                  "%*s    if (first) bits[%u] |= ((iv.a <= tmin && iv.b > tmin) ? 1u : 0u) << %u;\n"
-                 "%*s    if (iv.a > tmin) { uint64_t k = wodev::event_key_lo(iv.a, ka | iv.ma); if (k > after) "
-                 "win.insert(k); }\n"
-                 "%*s    if (iv.b > tmin && iv.b < wodev::kInf) { uint64_t k = wodev::event_key_lo(iv.b, kb | iv.mb); "
-                 "if (k > after) win.insert(k); }\n"
+                 "%*s    uint64_t k0 = wodev::event_key_lo(iv.a, ka | iv.ma), k1 = wodev::event_key_lo(iv.b, kb | iv.mb);\n"
+                 "%*s    if ((iv.a > tmin) & (k0 > after)) win.insert(k0);\n"
+                 "%*s    if ((iv.b > tmin) & (iv.b < wodev::kInf) & (k1 > after)) win.insert(k1);\n"
                  "%*s  }\n%*s}\n",
-                 indent, "", ord / 32, ord % 32, indent, "", indent, "", indent, "", indent, "");
+                 indent, "", ord / 32, ord % 32, indent, "", indent, "", indent, "", indent, "", indent, "");
             pc += 1 + cnt;
         } else {
             ++pc; /* binops: nothing to collect */
@@ -272,7 +275,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "      if (have && r != root) { wodev::hit_from_key(key, r, hit); return true; }\n"
              "      root = r;\n"
              "      if (win.k[0] == wodev::kEmptyKey) {\n"
-             "        if (!win.dropped) return false;\n"
+             "        if (!win.dropped()) return false;\n"
              "        after = key; win.clear(); collect = true; have = false;\n"
              "        continue;\n"
              "      }\n"

@@ -63,7 +63,6 @@ template <class Prog>
 __device__ __forceinline__ Ivl prim_interval(Prog prog, uint32_t pc, uint32_t count, F3 o, F3 d, F3& inv,
                                              bool& have_inv) {
     Ivl iv;
-    ivl_init(iv);
     for (uint32_t m = 0; m < count; ++m) {
         WoRec L = prog[pc + 1u + m];
         uint32_t kind = uni(L.op);
@@ -73,7 +72,10 @@ __device__ __forceinline__ Ivl prim_interval(Prog prog, uint32_t pc, uint32_t co
         }
         float la, lb;
         leaf_interval(L, kind, o, d, inv, la, lb);
-        ivl_meet(iv, la, lb, m);
+        if (m == 0u)
+            ivl_first(iv, la, lb);
+        else
+            ivl_meet(iv, la, lb, m);
     }
     return iv;
 }
@@ -216,7 +218,7 @@ struct InterpTracer {
                 return true;
             }
             root = r;
-            if (win.k[0] == kEmptyKey && win.dropped) {
+            if (win.k[0] == kEmptyKey && win.dropped()) {
                 // window exhausted but events were dropped: re-collect the events
                 // strictly after `key` (the membership state carries on)
                 win.clear();

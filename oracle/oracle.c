@@ -336,10 +336,12 @@ static int trace_ray(const WoRec* prog, uint32_t n, Scratch* s, const float o[3]
     const float tmin = WO_T_MIN;
     uint32_t nev = 0;
     for (uint32_t k = 0; k < s->nprims; ++k) {
-        /* convex primitive: intersection of the member spans; first extreme wins */
-        float lo = -INFINITY, hi = INFINITY;
+        /* convex primitive: intersection of the member spans, starting from the
+         * first member's span; the first member attaining the extreme wins */
+        float lo, hi;
         uint32_t mlo = 0, mhi = 0;
-        for (uint32_t m = 0; m < s->prims[k].count; ++m) {
+        leaf_span(&prog[s->prims[k].pc + 1u], o, d, &lo, &hi);
+        for (uint32_t m = 1; m < s->prims[k].count; ++m) {
             float a, b;
             leaf_span(&prog[s->prims[k].pc + 1u + m], o, d, &a, &b);
             if (a > lo) {
