@@ -299,9 +299,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "    float4* __restrict__ out, unsigned long long* __restrict__ seg_out) {\n"
          "  JitTracer tr;\n"
          "  tr.prog = prog;\n"
-         "  uint32_t lx, lrow;\n"
-         "  wodev::block_pixel(threadIdx.x, lx, lrow);\n"
-         "  wodev::pathtrace_pixel(tr, mats, fr, lx, lrow, local_rows, out, seg_out, threadIdx.x & 63u);\n"
+         "  wodev::pathtrace_block(tr, mats, fr, local_rows, out, seg_out);\n"
          "}\n");
     if (g.err || b.oom) {
         free(b.s);

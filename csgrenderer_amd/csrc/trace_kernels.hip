@@ -331,9 +331,7 @@ __global__ __launch_bounds__(kBlock) void pathtrace_kernel(const WoRec* __restri
     tr.ordpc = ws + lay.ordpc_off;
     tr.hib = ws + lay.hib_off;
     tr.lane = lane;
-    uint32_t lx, lrow;
-    block_pixel(tid, lx, lrow);
-    pathtrace_pixel(tr, mats, fr, lx, lrow, local_rows, out, seg_out, lane);
+    pathtrace_block(tr, mats, fr, local_rows, out, seg_out);
 }
 
 __global__ __launch_bounds__(kBlock) void assemble_kernel(const float4* __restrict__ gathered, float4* __restrict__ frame,

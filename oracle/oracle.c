@@ -177,10 +177,11 @@ static void rand_unit_vector(uint32_t* rng, float p[3]) {
 static void leaf_span(const WoRec* L, const float o[3], const float d[3], float* lo, float* hi) {
     if (L->op == WO_LEAF_SPHERE) {
         /* |o + t d - c|^2 = r^2 with |d| = 1, via the perpendicular foot l */
+        /* single-rounding fused multiply-adds in this order (fmaf) */
         float f[3] = {o[0] - L->f[0], o[1] - L->f[1], o[2] - L->f[2]};
-        float b = dot3(f, d);
-        float l[3] = {f[0] - b * d[0], f[1] - b * d[1], f[2] - b * d[2]};
-        float disc = L->f[3] - dot3(l, l);
+        float b = fmaf(f[2], d[2], fmaf(f[1], d[1], f[0] * d[0]));
+        float l[3] = {fmaf(-b, d[0], f[0]), fmaf(-b, d[1], f[1]), fmaf(-b, d[2], f[2])};
+        float disc = L->f[3] - fmaf(l[2], l[2], fmaf(l[1], l[1], l[0] * l[0]));
         if (disc < 0.0f) {
             *lo = INFINITY;
             *hi = -INFINITY;
@@ -414,6 +415,14 @@ static void sky_color(const float d[3], float c[3]) {
     c[2] = s + t * 1.0f;
 }
 
+/* Samples are summed as exact 32.32 fixed point, so a pixel's sum does not depend
+ * on the order its samples are added in (the GPU hands samples to whichever lane
+ * is free).  |r| >= 2^20 and NaN contribute 0. */
+static int64_t quantize_radiance(float r) { return fabsf(r) < 1048576.0f ? (int64_t)((double)r * 4294967296.0) : 0; }
+static float mean_radiance(int64_t sum, uint32_t spp) {
+    return (float)(((double)sum * (1.0 / 4294967296.0)) / (double)spp);
+}
+
 /* One pixel: spp samples of up to max_depth segments each. */
 static void shade_pixel(const WoRec* prog, uint32_t n, const WoMaterial* mats, uint32_t n_mats, const WoFrame* fr,
                         Scratch* s, uint32_t x, uint32_t y, float out[4], uint64_t* segs) {
@@ -423,9 +432,9 @@ static void shade_pixel(const WoRec* prog, uint32_t n, const WoMaterial* mats, u
     const uint32_t max_depth = normals ? 1u : fr->max_depth;
     const uint32_t W = fr->width, H = fr->height;
     const uint32_t pixel = y * W + x;
-    float sum[3] = {0.0f, 0.0f, 0.0f};
+    int64_t sum[3] = {0, 0, 0};
     if (spp == 0 || max_depth == 0) {
-        out[0] = out[1] = out[2] = 0.0f / (float)spp;
+        for (int i = 0; i < 3; ++i) out[i] = mean_radiance(0, spp);
         out[3] = 1.0f;
         return;
     }
@@ -547,9 +556,9 @@ static void shade_pixel(const WoRec* prog, uint32_t n, const WoMaterial* mats, u
                 d[i] = nd[i];
             }
         }
-        for (int i = 0; i < 3; ++i) sum[i] = sum[i] + rad[i];
+        for (int i = 0; i < 3; ++i) sum[i] += quantize_radiance(rad[i]);
     }
-    for (int i = 0; i < 3; ++i) out[i] = sum[i] / (float)spp;
+    for (int i = 0; i < 3; ++i) out[i] = mean_radiance(sum[i], spp);
     out[3] = 1.0f;
 }
 
