@@ -20,6 +20,15 @@
 #include <omp.h>
 #endif
 
+/* Analysis builds (tools/trace_stats.c) observe every trace: events collected,
+ * events swept up to the hit, hit or miss.  No-op in the oracle proper. */
+#ifndef ORACLE_TRACE_HOOK
+#define ORACLE_TRACE_HOOK(scratch, n_events, n_swept, hit) ((void)0)
+#endif
+#ifndef ORACLE_DEPTH_HOOK
+#define ORACLE_DEPTH_HOOK(depth) ((void)0)
+#endif
+
 /* ======================================================================== */
 /* Reference shader: src/wololo/renderer/ubershader1.frag                   */
 /* ======================================================================== */
@@ -360,7 +369,10 @@ static int trace_ray(const WoRec* prog, uint32_t n, Scratch* s, const float o[3]
         if (lo > tmin) s->ev[nev++].key = make_key(lo, k, 0u, mlo);
         if (hi > tmin && hi < INFINITY) s->ev[nev++].key = make_key(hi, k, 1u, mhi);
     }
-    if (nev == 0) return 0;
+    if (nev == 0) {
+        ORACLE_TRACE_HOOK(s, 0u, 0u, 0);
+        return 0;
+    }
     qsort(s->ev, nev, sizeof(Event), cmp_event);
     int root = eval_tree(prog, n, s->inside, s->stack);
     for (uint32_t i = 0; i < nev; ++i) {
@@ -379,10 +391,12 @@ static int trace_ray(const WoRec* prog, uint32_t n, Scratch* s, const float o[3]
             hit->type = (lo32 >> 11) & 1u;
             hit->member = lo32 & 2047u;
             hit->root_after = (uint32_t)r;
+            ORACLE_TRACE_HOOK(s, nev, i + 1u, 1);
             return 1;
         }
         root = r;
     }
+    ORACLE_TRACE_HOOK(s, nev, nev, 0);
     return 0;
 }
 
@@ -471,6 +485,7 @@ static void shade_pixel(const WoRec* prog, uint32_t n, const WoMaterial* mats, u
         for (uint32_t depth = 0; depth < max_depth; ++depth) {
             OHit h;
             ++*segs;
+            ORACLE_DEPTH_HOOK(depth);
             if (!trace_ray(prog, n, s, o, d, &h)) {
                 float sk[3];
                 sky_color(d, sk);
