@@ -191,7 +191,7 @@ def main():
         if args.pmc_json and os.path.exists(args.pmc_json):
             try:
                 pmc = json.load(open(args.pmc_json))
-                key = f"{args.scene}:{W}x{H}:{params.spp}:{world}"
+                key = f"{args.scene}:{W}x{H}:{params.spp}:{world}:{roof.get('trace_path', 'ubershader')}"
                 if key in pmc:
                     roof["traffic"] = pmc[key]
             except Exception as e:  # report, don't fail the bench

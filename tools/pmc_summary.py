@@ -31,7 +31,7 @@ def counters(d, name):
     files, rows = _rows(os.path.join(d, name), "*counter_collection.csv")
     per = {}
     for r in rows:
-        if not r["Kernel_Name"].startswith(KERNELS):
+        if not any(k in r["Kernel_Name"] for k in KERNELS):
             continue
         per.setdefault(r["Counter_Name"], {}).setdefault(r["Dispatch_Id"], 0.0)
         per[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
@@ -48,7 +48,7 @@ def main():
     res = {}
     kfiles, krows = _rows(os.path.join(a.dir, "kstats"), "*kernel_stats.csv")
     for r in krows:
-        if r["Name"].startswith(KERNELS):
+        if any(k in r["Name"] for k in KERNELS):
             res["kernel"] = r["Name"]
             res["calls"] = int(r["Calls"])
             res["avg_ms"] = float(r["AverageNs"]) / 1e6
