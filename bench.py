@@ -45,7 +45,10 @@ def parse():
     ap.add_argument("--tile-rows", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--jit", type=int, default=1, help="1: scene-specialised kernel (auto), 0: interpreter kernel")
+    ap.add_argument("--tracer", default=os.environ.get("WOLOLO_TRACER", "auto"),
+                    choices=["auto", "interpreter", "jit", "lanes"],
+                    help="path-tracer kernel (renderer_ext.h Wo_Tracer); results are identical")
+    ap.add_argument("--jit", type=int, default=None, help="legacy: 0 = --tracer interpreter")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo stages the gather through host memory (for rehearsing N>1 ranks on one GPU)")
     ap.add_argument("--verify", action="store_true",
@@ -92,7 +95,7 @@ def main():
     if args.spp:
         over["spp"] = args.spp
     params = info.params(**over)
-    r.set_jit(args.jit)
+    r.set_tracer("interpreter" if args.jit == 0 else args.tracer)
     W, H, T = params.width, params.height, args.tile_rows
     lr = wl.local_rows(H, T, world)
     out = torch.empty((lr, W, 4), dtype=torch.float32, device=dev)
@@ -175,7 +178,8 @@ def main():
             achieved_tf = flop_launch / (k_ms * 1e-3) / 1e12
             roof = {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4), "traffic": None,
-                    "kernel": "wo_jit_pathtrace" if r.trace_path() == "jit" else "pathtrace_kernel",
+                    "kernel": {"jit": "wo_jit_pathtrace", "lanes": "pathtrace_lanes_kernel"}.get(r.trace_path(),
+                                                                                              "pathtrace_kernel"),
                     "kernel_ms": round(k_ms, 4),
                     "flop_per_segment": info.flop_per_segment,
                     "segments_per_launch": segs_local // steps, "trace_path": r.trace_path()}

@@ -102,7 +102,12 @@ Wo_Renderer* wo_renderer_new(Wo_App* app, char const* name, size_t max_node_coun
     r->dirty = 1;
     {
         const char* j = getenv("WOLOLO_JIT");
-        r->jit_mode = (j && strcmp(j, "0") == 0) ? 0 : 1;
+        const char* t = getenv("WOLOLO_TRACER");
+        r->tracer = WO_TRACER_AUTO;
+        if (j && strcmp(j, "0") == 0) r->tracer = WO_TRACER_INTERPRETER;
+        if (t && strcmp(t, "interpreter") == 0) r->tracer = WO_TRACER_INTERPRETER;
+        if (t && strcmp(t, "jit") == 0) r->tracer = WO_TRACER_JIT;
+        if (t && strcmp(t, "lanes") == 0) r->tracer = WO_TRACER_LANES;
     }
     r->device = -1;
 
@@ -353,10 +358,19 @@ static int sync_device(Wo_Renderer* r) {
         }
         r->dev_stale = 0;
         r->jit_loaded = 0;
-        uint32_t max_prims = 256;
+        r->lanes_loaded = 0;
+        uint32_t max_prims = 256, lanes_min = 64;
         const char* mp = getenv("WOLOLO_JIT_MAX_PRIMS");
         if (mp && *mp) max_prims = (uint32_t)strtoul(mp, NULL, 10);
-        if (r->jit_mode && r->n_prims > 0 && r->n_prims <= max_prims) {
+        const char* lm = getenv("WOLOLO_LANES_MIN_PRIMS");
+        if (lm && *lm) lanes_min = (uint32_t)strtoul(lm, NULL, 10);
+        int lanes_ok = wo_dev_lanes_available(r->dev);
+        int want_lanes = lanes_ok && (r->tracer == WO_TRACER_LANES ||
+                                      (r->tracer == WO_TRACER_AUTO && r->n_prims > lanes_min));
+        int want_jit = !want_lanes && r->tracer != WO_TRACER_INTERPRETER && r->n_prims > 0 && r->n_prims <= max_prims;
+        wo_dev_set_lanes(r->dev, want_lanes);
+        r->lanes_loaded = want_lanes;
+        if (want_jit) {
             char* src = wo_generate_jit_source(r->prog, r->n_recs, r->n_prims);
             if (!src) {
                 fprintf(stderr, WO_LOG_PREFIX " scene specialisation: source generation failed; using the interpreter\n");
@@ -372,11 +386,15 @@ static int sync_device(Wo_Renderer* r) {
     return 0;
 }
 
-void wo_renderer_set_jit(Wo_Renderer* r, int mode) {
-    if (r->jit_mode != (mode ? 1 : 0)) {
-        r->jit_mode = mode ? 1 : 0;
+void wo_renderer_set_tracer(Wo_Renderer* r, Wo_Tracer tracer) {
+    if (r->tracer != (int)tracer) {
+        r->tracer = (int)tracer;
         r->dev_stale = 1;
     }
+}
+
+void wo_renderer_set_jit(Wo_Renderer* r, int mode) {
+    wo_renderer_set_tracer(r, mode ? WO_TRACER_AUTO : WO_TRACER_INTERPRETER);
 }
 
 char* wo_renderer_jit_source(Wo_Renderer* r) {
@@ -388,7 +406,7 @@ void wo_free(void* p) { free(p); }
 
 char const* wo_renderer_trace_path(Wo_Renderer* r) {
     if (!r->dev) return "none";
-    return r->jit_loaded ? "jit" : "interpreter";
+    return r->jit_loaded ? "jit" : r->lanes_loaded ? "lanes" : "interpreter";
 }
 
 int wo_renderer_render_f32(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba) {

@@ -17,7 +17,9 @@
  *   3. operands are emitted larger-stack-need first (Sethi-Ullman), so the
  *      kernel's 32-bit evaluation stack never overflows; DIFF becomes RDIFF
  *      when the subtrahend is emitted first;
- *   4. subtrees with >= 2 leaves (WOLOLO_BOUND_MIN_LEAVES) and a finite extent get a conservative
+ *   4. every maximal union cluster is re-bracketed as a bounding-volume hierarchy
+ *      over its operands (regroup; union is associative and commutative);
+ *   5. subtrees with >= 2 leaves (WOLOLO_BOUND_MIN_LEAVES) and a finite extent get a conservative
  *      WO_OP_BOUND sphere so a wave whose rays all miss can skip them.
  */
 #include <math.h>
@@ -59,6 +61,7 @@ typedef struct Ctx {
     size_t errlen;
     int failed;
     int bound_min_leaves; /* smallest subtree (in leaves) that gets a BOUND record */
+    int regroup_unions;   /* rebuild union clusters as a BVH (WOLOLO_REGROUP_UNIONS=0: keep the scene's) */
 } Ctx;
 
 #define MAX_EXPANDED_NODES (1u << 21)
@@ -304,6 +307,31 @@ static void collect_members(Ctx* c, int id, int* out, int* n) {
     collect_members(c, e->r, out, n);
 }
 
+/* Operands of the union cluster under `id` (already analysed, bounded). */
+static void union_atoms_box(Ctx* c, int id, double lo[3], double hi[3]) {
+    const ENode* e = &c->e[id];
+    if (e->kind == E_UNION && !e->convex) {
+        union_atoms_box(c, e->l, lo, hi);
+        union_atoms_box(c, e->r, lo, hi);
+        return;
+    }
+    for (int k = 0; k < 3; ++k) {
+        if (e->bc[k] - e->br < lo[k]) lo[k] = e->bc[k] - e->br;
+        if (e->bc[k] + e->br > hi[k]) hi[k] = e->bc[k] + e->br;
+    }
+}
+static void union_atoms_radius(Ctx* c, int id, const double oc[3], double* orad) {
+    const ENode* e = &c->e[id];
+    if (e->kind == E_UNION && !e->convex) {
+        union_atoms_radius(c, e->l, oc, orad);
+        union_atoms_radius(c, e->r, oc, orad);
+        return;
+    }
+    double d[3] = {e->bc[0] - oc[0], e->bc[1] - oc[1], e->bc[2] - oc[2]};
+    double r = sqrt(dot3d(d, d)) + e->br;
+    if (r > *orad) *orad = r;
+}
+
 /* Post-order analysis: convexity, stack need, leaf count, bounds. */
 static void analyse(Ctx* c, int id) {
     ENode* e = &c->e[id];
@@ -387,6 +415,19 @@ static void analyse(Ctx* c, int id) {
         if (L->bounded && R->bounded) {
             enclose(L->bc, L->br, R->bc, R->br, e->bc, &e->br);
             e->bounded = 1;
+            /* pairwise enclosing spheres grow loose with depth: also try the sphere
+             * around the AABB of the cluster's operand spheres, keep the smaller */
+            if (e->leaves <= 4096) {
+                double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                union_atoms_box(c, id, lo, hi);
+                double oc[3], orad = 0.0;
+                for (int k = 0; k < 3; ++k) oc[k] = 0.5 * (lo[k] + hi[k]);
+                union_atoms_radius(c, id, oc, &orad);
+                if (orad < e->br) {
+                    memcpy(e->bc, oc, sizeof oc);
+                    e->br = orad;
+                }
+            }
         }
     } else if (e->kind == E_INTER) {
         const ENode* pick = NULL;
@@ -404,6 +445,129 @@ static void analyse(Ctx* c, int id) {
             e->bounded = 1;
         }
     }
+}
+
+/* ---- union regrouping ---- */
+
+/* Union is associative and commutative, so every maximal union cluster (a union
+ * node and its union descendants) may be re-bracketed freely.  The scene's own
+ * bracketing follows the order the caller added nodes in (the RTIOW cover adds
+ * its spheres row by row: a balanced union of such a list groups long thin
+ * strips whose bounding spheres are huge).  The cluster's operands are rebuilt
+ * into a bounding-volume hierarchy instead: median split of the operands'
+ * bounding-sphere centres along the longest axis, unbounded operands (half-
+ * spaces) unioned on top.  The set the program describes is unchanged. */
+typedef struct SortKey {
+    double key;
+    int id;
+} SortKey;
+
+static int cmp_sortkey(const void* a, const void* b) {
+    const SortKey* x = (const SortKey*)a;
+    const SortKey* y = (const SortKey*)b;
+    if (x->key < y->key) return -1;
+    if (x->key > y->key) return 1;
+    return x->id < y->id ? -1 : x->id > y->id;
+}
+
+static int union_of(Ctx* c, int l, int r) {
+    int id = new_enode(c);
+    if (id < 0) return -1;
+    c->e[id].kind = E_UNION;
+    c->e[id].l = l;
+    c->e[id].r = r;
+    return id;
+}
+
+static int bvh_build(Ctx* c, int* ids, int n, SortKey* tmp) {
+    if (n == 1) return ids[0];
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) {
+            double v = c->e[ids[i]].bc[k];
+            if (v < lo[k]) lo[k] = v;
+            if (v > hi[k]) hi[k] = v;
+        }
+    int axis = 0;
+    for (int k = 1; k < 3; ++k)
+        if (hi[k] - lo[k] > hi[axis] - lo[axis]) axis = k;
+    for (int i = 0; i < n; ++i) {
+        tmp[i].key = c->e[ids[i]].bc[axis];
+        tmp[i].id = ids[i];
+    }
+    qsort(tmp, (size_t)n, sizeof(SortKey), cmp_sortkey);
+    for (int i = 0; i < n; ++i) ids[i] = tmp[i].id;
+    int h = n / 2;
+    int l = bvh_build(c, ids, h, tmp);
+    int r = bvh_build(c, ids + h, n - h, tmp);
+    if (l < 0 || r < 0) return -1;
+    return union_of(c, l, r);
+}
+
+static int regroup(Ctx* c, int id);
+
+static int gather_union_operands(Ctx* c, int id, int** ops, int* n, int* cap) {
+    if (c->e[id].kind == E_UNION) {
+        int l = c->e[id].l, r = c->e[id].r;
+        if (gather_union_operands(c, l, ops, n, cap)) return -1;
+        return gather_union_operands(c, r, ops, n, cap);
+    }
+    if (*n == *cap) {
+        int nc = *cap ? *cap * 2 : 16;
+        int* no = (int*)realloc(*ops, sizeof(int) * (size_t)nc);
+        if (!no) {
+            fail(c, "out of host memory");
+            return -1;
+        }
+        *ops = no;
+        *cap = nc;
+    }
+    (*ops)[(*n)++] = id;
+    return 0;
+}
+
+static int regroup(Ctx* c, int id) {
+    if (c->failed) return -1;
+    int kind = c->e[id].kind;
+    if (kind == E_SPHERE || kind == E_HALF) return id;
+    if (kind != E_UNION) {
+        int l = regroup(c, c->e[id].l);
+        int r = regroup(c, c->e[id].r);
+        if (l < 0 || r < 0) return -1;
+        c->e[id].l = l;
+        c->e[id].r = r;
+        return id;
+    }
+    int *ops = NULL, n = 0, cap = 0;
+    if (gather_union_operands(c, id, &ops, &n, &cap)) {
+        free(ops);
+        return -1;
+    }
+    int nb = 0;
+    for (int i = 0; i < n; ++i) {
+        ops[i] = regroup(c, ops[i]);
+        if (ops[i] < 0) {
+            free(ops);
+            return -1;
+        }
+        analyse(c, ops[i]);
+        if (c->e[ops[i]].bounded) { /* bounded operands first, in their original order */
+            int t = ops[i];
+            memmove(ops + nb + 1, ops + nb, sizeof(int) * (size_t)(i - nb));
+            ops[nb++] = t;
+        }
+    }
+    SortKey* tmp = (SortKey*)malloc(sizeof(SortKey) * (size_t)n);
+    if (!tmp) {
+        free(ops);
+        fail(c, "out of host memory");
+        return -1;
+    }
+    int root = nb ? bvh_build(c, ops, nb, tmp) : -1;
+    for (int i = nb; i < n && !c->failed; ++i) root = root < 0 ? ops[i] : union_of(c, root, ops[i]);
+    free(tmp);
+    free(ops);
+    return c->failed ? -1 : root;
 }
 
 /* ---- emission ---- */
@@ -471,6 +635,7 @@ static void emit(Ctx* c, int id, double outer_r) {
         double cn = sqrt(dot3d(e->bc, e->bc));
         double R = e->br * (1.0 + 1e-4) + 1e-5 * (cn + e->br) + 1e-6;
         b->op = WO_OP_BOUND;
+        b->u1 = (uint32_t)e->leaves;
         b->f[0] = (float)e->bc[0];
         b->f[1] = (float)e->bc[1];
         b->f[2] = (float)e->bc[2];
@@ -526,6 +691,11 @@ int wo_compile_scene(Wo_Renderer* r, char* err, size_t errlen) {
     c.err = err;
     c.errlen = errlen;
     c.bound_min_leaves = 2;
+    c.regroup_unions = 1;
+    {
+        const char* v = getenv("WOLOLO_REGROUP_UNIONS");
+        if (v && strcmp(v, "0") == 0) c.regroup_unions = 0;
+    }
     {
         const char* v = getenv("WOLOLO_BOUND_MIN_LEAVES");
         if (v && *v) c.bound_min_leaves = atoi(v) > 1 ? atoi(v) : 2;
@@ -548,6 +718,7 @@ int wo_compile_scene(Wo_Renderer* r, char* err, size_t errlen) {
     }
     if (!c.failed && nroots > 0) {
         int root = make_union(&c, roots, nroots);
+        if (root >= 0 && !c.failed && c.regroup_unions) root = regroup(&c, root);
         if (root >= 0 && !c.failed) {
             analyse(&c, root);
             if (c.e[root].need > 31) fail(&c, "CSG tree needs an evaluation stack deeper than 31");

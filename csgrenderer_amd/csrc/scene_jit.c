@@ -80,6 +80,7 @@ static void emit_consts(Buf* b, int indent, const char* type, const char* names[
 typedef struct Gen {
     const WoRec* prog;
     uint32_t n;
+    uint32_t bound_min_leaves; /* smaller BOUND records are not tested (inlined) */
     Buf* b;
     uint32_t nbound;  /* BOUND counter (cull flag names) */
     uint32_t nval;    /* value counter (eval temporaries) */
@@ -91,7 +92,9 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
     uint32_t pc = start;
     while (pc < end && !g->err) {
         const WoRec* r = &g->prog[pc];
-        if (r->op == WO_OP_BOUND) {
+        if (r->op == WO_OP_BOUND && r->u1 < g->bound_min_leaves) {
+            ++pc; /* too small to pay for a wave-level test: the subtree is emitted inline */
+        } else if (r->op == WO_OP_BOUND) {
             static const char* nb[5] = {"bc0", "bc1", "bc2", "bc3", "bc4"};
             uint32_t vb[5];
             for (int i = 0; i < 5; ++i) vb[i] = fbits(r->f[i]);
@@ -163,7 +166,9 @@ static uint32_t gen_eval(Gen* g, uint32_t start, uint32_t end, int indent) {
     uint32_t pc = start;
     while (pc < end && !g->err) {
         const WoRec* r = &g->prog[pc];
-        if (r->op == WO_OP_BOUND) {
+        if (r->op == WO_OP_BOUND && r->u1 < g->bound_min_leaves) {
+            ++pc;
+        } else if (r->op == WO_OP_BOUND) {
             uint32_t k = g->nbound++;
             uint32_t v = g->nval++;
             bput(g->b, "%*suint32_t v%u;\n%*sif (!(cull[%u] & %uu)) {\n", indent, "", v, indent, "", k / 32,
@@ -220,8 +225,15 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     g.n = n_recs;
     g.b = &b;
     uint32_t nw = n_prims ? (n_prims + 31u) / 32u : 1u;
+    /* Wave-level BOUND tests pay only for larger subtrees (measured: csg32 6.54 ms
+     * testing subtrees of >= 8 leaves vs 6.94 ms testing every BOUND record). */
+    g.bound_min_leaves = 8;
+    {
+        const char* v = getenv("WOLOLO_JIT_BOUND_MIN_LEAVES");
+        if (v && *v) g.bound_min_leaves = (uint32_t)strtoul(v, NULL, 10);
+    }
     uint32_t nbounds = 0;
-    for (uint32_t i = 0; i < n_recs; ++i) nbounds += prog[i].op == WO_OP_BOUND;
+    for (uint32_t i = 0; i < n_recs; ++i) nbounds += prog[i].op == WO_OP_BOUND && prog[i].u1 >= g.bound_min_leaves;
 
     bput(&b, "// generated by scene_jit.c: %u records, %u primitives, %u bounds\n", n_recs, n_prims, nbounds);
     bput(&b, "#include \"wo_device_common.h\"\n\n");

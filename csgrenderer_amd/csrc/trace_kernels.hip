@@ -253,6 +253,137 @@ struct InterpTracer {
 };
 
 // ---------------------------------------------------------------------------
+// Lane traversal, for programs whose every binop is a UNION (scenes like the
+// RTIOW cover: hundreds of primitives, no CSG).  Each lane walks the BOUND
+// hierarchy on its own (stackless: a missed BOUND jumps to its skip target),
+// so a wave costs the LONGEST lane's walk instead of the UNION of its lanes'
+// walks -- the difference that matters for incoherent bounce rays.  The trav
+// table is the program with the binop records dropped (host: build_trav).
+//
+// Union semantics need no tree evaluation: the root is inside iff the count
+// of primitives containing the point is > 0; an entry event adds one, an exit
+// removes one.  A BOUND whose near end (tca - R, with slack) lies beyond the
+// nearest event collected so far is pruned; the sweep treats the smallest
+// pruned near end as a barrier (`kcut`): reaching it re-collects after the
+// last processed event, exactly as an overflowing window does.  Results are
+// the general algorithm's, bit for bit.
+// ---------------------------------------------------------------------------
+struct LaneTracer {
+    const WoRec* __restrict__ prog;   // full program (hit leaves)
+    const WoRec* __restrict__ trav;   // BOUND / PRIM+leaves, binops dropped
+    const uint32_t* __restrict__ ordpc;
+    uint32_t ntrav;
+
+    __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const { return prog[ordpc[h.ord] + 1u + h.member]; }
+
+    __device__ __forceinline__ bool trace(F3 o, F3 d, Hit& hit) {
+        const float tmin = WO_T_MIN;
+        F3 inv = f3(0.0f, 0.0f, 0.0f);
+        bool have_inv = false;
+        Window win;
+        int cnt = 0;  // primitives containing the current point
+        uint32_t root = 0;
+        uint64_t after = 0ull, key = 0ull;
+        bool first = true;
+        for (;;) {
+            win.clear();
+            uint64_t kcut = kEmptyKey;
+            uint32_t pc = 0;
+            while (pc < ntrav) {
+                WoRec r = trav[pc];
+                if (r.op == WO_OP_BOUND) {
+                    float ox = r.f[0] - o.x, oy = r.f[1] - o.y, oz = r.f[2] - o.z;
+                    float tca = __builtin_fmaf(oz, d.z, __builtin_fmaf(oy, d.y, ox * d.x));
+                    float lx = __builtin_fmaf(-tca, d.x, ox), ly = __builtin_fmaf(-tca, d.y, oy),
+                          lz = __builtin_fmaf(-tca, d.z, oz);
+                    float d2 = __builtin_fmaf(lz, lz, __builtin_fmaf(ly, ly, lx * lx));
+                    bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, r.f[3])) || (tca + r.f[4] < 0.0f);
+                    // near end of the sphere along the ray, rounded down generously
+                    float lo = (tca - r.f[4]) - 1e-5f * (fabsf(tca) + r.f[4]);
+                    float tnear = __uint_as_float((uint32_t)(win.k[0] >> 32));  // +inf bits pattern when empty
+                    bool prune = !miss && win.k[0] != kEmptyKey && lo > tnear;
+                    if (prune) {
+                        uint64_t kc = (uint64_t)__float_as_uint(lo) << 32;
+                        kcut = kc < kcut ? kc : kcut;
+                    }
+                    pc = (miss || prune) ? r.u0 : pc + 1u;
+                } else {
+                    const uint32_t count = r.u0, ord = r.u1;
+                    Ivl iv;
+                    for (uint32_t m = 0; m < count; ++m) {
+                        WoRec L = trav[pc + 1u + m];
+                        float la, lb;
+                        if (L.op == WO_LEAF_SPHERE) {
+                            sphere_interval(L.f[0], L.f[1], L.f[2], L.f[3], o, d, la, lb);
+                        } else if (L.u1 != 0u) {
+                            if (!have_inv) {
+                                inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                                have_inv = true;
+                            }
+                            uint32_t a = L.u1 - 1u;
+                            halfspace_axis_interval(a == 0u ? L.f[0] : (a == 1u ? L.f[1] : L.f[2]), L.f[3],
+                                                    pick3(o, a), pick3(d, a), pick3(inv, a), la, lb);
+                        } else {
+                            halfspace_interval(L.f[0], L.f[1], L.f[2], L.f[3], o, d, la, lb);
+                        }
+                        if (m == 0u)
+                            ivl_first(iv, la, lb);
+                        else
+                            ivl_meet(iv, la, lb, m);
+                    }
+                    if (!(iv.a > iv.b)) {
+                        if (first && iv.a <= tmin && iv.b > tmin) ++cnt;
+                        uint64_t k0 = event_key(iv.a, ord, 0u, iv.ma), k1 = event_key(iv.b, ord, 1u, iv.mb);
+                        if (iv.a > tmin && k0 > after) win.insert(k0);
+                        if (iv.b > tmin && iv.b < kInf && k1 > after) win.insert(k1);
+                    }
+                    pc += 1u + count;
+                }
+            }
+            if (first) {
+                first = false;
+                if (win.k[0] == kEmptyKey) return false;
+                root = cnt > 0 ? 1u : 0u;
+            }
+            // sweep up to the barrier
+            bool again = false;
+            for (;;) {
+                uint64_t nk = win.k[0];
+                if (nk == kEmptyKey || nk >= kcut) {
+                    again = win.dropped() || kcut != kEmptyKey;
+                    break;
+                }
+                key = win.pop();
+                cnt += ((uint32_t)key & (1u << 11)) ? -1 : 1;
+                uint32_t rv = cnt > 0 ? 1u : 0u;
+                if (rv != root) {
+                    hit_from_key(key, rv, hit);
+                    return true;
+                }
+                root = rv;
+            }
+            if (!again) return false;
+            after = key;
+        }
+    }
+};
+
+__global__ __launch_bounds__(kBlock) void pathtrace_lanes_kernel(const WoRec* __restrict__ prog,
+                                                                 const WoRec* __restrict__ trav,
+                                                                 const uint32_t* __restrict__ ordpc,
+                                                                 const WoMaterial* __restrict__ mats, WoFrame fr,
+                                                                 uint32_t ntrav, uint32_t local_rows,
+                                                                 float4* __restrict__ out,
+                                                                 unsigned long long* __restrict__ seg_out) {
+    LaneTracer tr;
+    tr.prog = prog;
+    tr.trav = trav;
+    tr.ordpc = ordpc;
+    tr.ntrav = ntrav;
+    pathtrace_block(tr, mats, fr, local_rows, out, seg_out);
+}
+
+// ---------------------------------------------------------------------------
 // ubershader1.frag restated (ref ubershader1.frag:19-163).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void ubershader_kernel(WoFrame fr, uint32_t local_rows, float4* __restrict__ out) {
@@ -363,6 +494,14 @@ struct WoDev {
     float4* d_frame;
     size_t frame_cap;
     hipStream_t stream;
+    // lane traversal (union-only programs): program without binops + ordinal -> pc
+    WoRec* d_trav;
+    size_t trav_cap;
+    uint32_t* d_ordpc;
+    size_t ordpc_cap;
+    uint32_t n_trav;
+    bool union_only;
+    bool lanes_on;
     // scene-specialised kernel (hiprtc)
     hipModule_t jit_module;
     hipFunction_t jit_fn;
@@ -422,6 +561,8 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
     if (dev->d_prog) (void)hipFree(dev->d_prog);
     if (dev->d_mats) (void)hipFree(dev->d_mats);
     if (dev->d_frame) (void)hipFree(dev->d_frame);
+    if (dev->d_trav) (void)hipFree(dev->d_trav);
+    if (dev->d_ordpc) (void)hipFree(dev->d_ordpc);
     if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
     (void)hipStreamDestroy(dev->stream);
     delete dev;
@@ -440,6 +581,58 @@ static int ensure_buffer(T** p, size_t* cap, size_t bytes, char* err, size_t err
         return -1;
     }
     *cap = alloc;
+    return 0;
+}
+
+// The lane tracer's table: the program minus its binop records, BOUND skip
+// targets renumbered; plus ordinal -> program pc for the hit leaf.  Built only
+// for union-only programs (otherwise n_trav = 0 and the lane kernel is unused).
+static int build_trav(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n_prims, char* err, size_t errlen) {
+    dev->n_trav = 0;
+    dev->union_only = false;
+    bool union_only = n_prims > 0;
+    for (uint32_t pc = 0; pc < n_recs && union_only;) {
+        uint32_t op = prog[pc].op;
+        if (op == WO_OP_PRIM) {
+            pc += 1u + prog[pc].u0;
+        } else {
+            if (op != WO_OP_UNION && op != WO_OP_BOUND) union_only = false;
+            ++pc;
+        }
+    }
+    if (!union_only) return 0;
+    std::vector<WoRec> trav;
+    std::vector<uint32_t> map(n_recs + 1u, 0u), ordpc(n_prims, 0u);
+    trav.reserve(n_recs);
+    for (uint32_t pc = 0; pc < n_recs;) {
+        const WoRec& r = prog[pc];
+        map[pc] = (uint32_t)trav.size();
+        if (r.op == WO_OP_PRIM) {
+            if (r.u1 < n_prims) ordpc[r.u1] = pc;
+            for (uint32_t m = 0; m <= r.u0; ++m) {
+                if (m) map[pc + m] = (uint32_t)trav.size();
+                trav.push_back(prog[pc + m]);
+            }
+            pc += 1u + r.u0;
+        } else {
+            if (r.op == WO_OP_BOUND) trav.push_back(r);
+            ++pc;
+        }
+    }
+    map[n_recs] = (uint32_t)trav.size();
+    for (WoRec& r : trav)
+        if (r.op == WO_OP_BOUND) r.u0 = r.u0 <= n_recs ? map[r.u0] : (uint32_t)trav.size();
+    if (ensure_buffer(&dev->d_trav, &dev->trav_cap, trav.size() * sizeof(WoRec), err, errlen)) return -1;
+    if (ensure_buffer(&dev->d_ordpc, &dev->ordpc_cap, (size_t)n_prims * sizeof(uint32_t), err, errlen)) return -1;
+    hipError_t e = hipMemcpy(dev->d_trav, trav.data(), trav.size() * sizeof(WoRec), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(dev->d_ordpc, ordpc.data(), (size_t)n_prims * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipMemcpy(traversal table)", e);
+        return -1;
+    }
+    dev->n_trav = (uint32_t)trav.size();
+    dev->union_only = true;
     return 0;
 }
 
@@ -469,7 +662,7 @@ extern "C" int wo_dev_upload_scene(WoDev* dev, WoRec const* prog, uint32_t n_rec
     dev->n_recs = n_recs;
     dev->n_prims = n_prims;
     dev->n_mats = n_mats;
-    return 0;
+    return build_trav(dev, prog, n_recs, n_prims, err, errlen);
 }
 
 // ---- scene-specialised kernels (hiprtc) ----
@@ -591,6 +784,10 @@ extern "C" int wo_jit_compile_check(const char* src, const char* arch, char* err
 }
 
 extern "C" int wo_dev_jit_active(WoDev* dev) { return dev && dev->jit_fn ? 1 : 0; }
+extern "C" int wo_dev_lanes_available(WoDev* dev) { return dev && dev->union_only ? 1 : 0; }
+extern "C" void wo_dev_set_lanes(WoDev* dev, int on) {
+    if (dev) dev->lanes_on = on != 0;
+}
 extern "C" double wo_dev_jit_compile_sec(WoDev* dev) { return dev ? dev->jit_compile_sec : 0.0; }
 
 static const size_t kLdsBudget = 64u * 1024u;
@@ -625,7 +822,10 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
             return -1;
         }
         dim3 grid((fr.width + kPtTile - 1) / kPtTile, (local_rows + kPtTile - 1) / kPtTile);
-        if (dev->jit_fn) {
+        if (dev->lanes_on && dev->union_only && !dev->jit_fn) {
+            hipLaunchKernelGGL(pathtrace_lanes_kernel, grid, dim3(kBlock), 0, stream, dev->d_prog, dev->d_trav,
+                               dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, d_segments);
+        } else if (dev->jit_fn) {
             const WoRec* p = dev->d_prog;
             const WoMaterial* m = dev->d_mats;
             unsigned long long* s = d_segments;

@@ -33,6 +33,9 @@ int wo_dev_upload_scene(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t
  * NORMALS frames launch it instead of the interpreter kernel. */
 int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t errlen);
 int wo_dev_jit_active(WoDev* dev);
+/* Lane traversal kernel (union-only programs, see trace_kernels.hip). */
+int wo_dev_lanes_available(WoDev* dev);
+void wo_dev_set_lanes(WoDev* dev, int on);
 double wo_dev_jit_compile_sec(WoDev* dev);
 /* Launch the frame's kernel for this rank's tiles into d_out on `stream` (async). */
 int wo_dev_launch(WoDev* dev, WoFrame const* frame, void* d_out, void* stream,

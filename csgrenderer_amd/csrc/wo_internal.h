@@ -66,8 +66,9 @@ struct Wo_Renderer {
     int device;         /* -1: device-less (tests only) */
     WoDev* dev;
 
-    int jit_mode;       /* 0 off, 1 auto (scenes up to WOLOLO_JIT_MAX_PRIMS primitives) */
+    int tracer;         /* Wo_Tracer */
     int jit_loaded;     /* the device runs the scene-specialised kernel */
+    int lanes_loaded;   /* the device runs the lane-traversal kernel */
 
     float* host_frame;
     size_t host_frame_cap;

@@ -23,6 +23,8 @@ WO_OP_PRIM, WO_OP_UNION, WO_OP_INTER, WO_OP_DIFF, WO_OP_RDIFF, WO_OP_BOUND = 1, 
 WO_LEAF_SPHERE, WO_LEAF_HALFSPACE = 16, 17
 WO_MAT_LAMBERTIAN, WO_MAT_METAL, WO_MAT_DIELECTRIC = 0, 1, 2
 MODE_UBERSHADER_RT1, MODE_DEBUG_ST, MODE_PATHTRACE, MODE_NORMALS = 0, 1, 2, 3
+TRACER_AUTO, TRACER_INTERPRETER, TRACER_JIT, TRACER_LANES = 0, 1, 2, 3
+TRACERS = {"auto": TRACER_AUTO, "interpreter": TRACER_INTERPRETER, "jit": TRACER_JIT, "lanes": TRACER_LANES}
 WO_T_MIN = 1.0e-3
 WO_NODE_INVALID = 0xFFFFFFFF
 
@@ -109,6 +111,7 @@ SIGNATURES = {
     "wo_renderer_frame_desc": (c_int, [c_void_p, POINTER(RenderParams), c_uint32, c_uint32, c_uint32,
                                        POINTER(WoFrame)]),
     "wo_renderer_set_jit": (None, [c_void_p, c_int]),
+    "wo_renderer_set_tracer": (None, [c_void_p, c_int]),
     "wo_renderer_trace_path": (c_char_p, [c_void_p]),
     "wo_renderer_jit_source": (c_void_p, [c_void_p]),
     "wo_jit_compile_check": (c_int, [c_char_p, c_char_p, c_char_p, c_size_t]),
@@ -261,6 +264,12 @@ class Renderer:
 
     def set_jit(self, mode: int):
         self.lib.wo_renderer_set_jit(self.ptr, int(mode))
+
+    def set_tracer(self, tracer):
+        """TRACER_AUTO / _INTERPRETER / _JIT / _LANES, or the names "auto", "interpreter", "jit", "lanes"."""
+        if isinstance(tracer, str):
+            tracer = TRACERS[tracer]
+        self.lib.wo_renderer_set_tracer(self.ptr, int(tracer))
 
     def trace_path(self) -> str:
         return self.lib.wo_renderer_trace_path(self.ptr).decode()

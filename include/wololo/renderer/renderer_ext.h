@@ -89,12 +89,28 @@ WoMaterial const* wo_renderer_materials(Wo_Renderer* r, uint32_t* n_materials);
 int wo_renderer_frame_desc(Wo_Renderer* r, Wo_RenderParams const* params, uint32_t tile_rows,
                            uint32_t rank, uint32_t nranks, WoFrame* out);
 
-/* Scene-specialised kernels: 0 = always use the interpreter kernel, 1 = auto
- * (default: specialise scenes of up to WOLOLO_JIT_MAX_PRIMS primitives, default
- * 256, compiled with hiprtc at scene upload; WOLOLO_JIT=0 in the environment
- * turns it off).  Takes effect at the next render. */
+/* Path-tracer kernel selection (results are identical; only speed differs).
+ *   AUTO         union-only scenes of more than WOLOLO_LANES_MIN_PRIMS (64)
+ *                primitives -> LANES; else scenes of up to WOLOLO_JIT_MAX_PRIMS
+ *                (256) primitives -> JIT; else INTERPRETER.
+ *   INTERPRETER  the postfix-program interpreter kernel.
+ *   JIT          the scene-specialised kernel, compiled with hiprtc at scene
+ *                upload, for scenes of up to WOLOLO_JIT_MAX_PRIMS primitives
+ *                (else, or if compilation fails, the interpreter).
+ *   LANES        per-lane BOUND traversal, for union-only scenes (others fall
+ *                back to AUTO's choice).
+ * Environment: WOLOLO_TRACER=auto|interpreter|jit|lanes sets the initial value;
+ * WOLOLO_JIT=0 means interpreter.  Takes effect at the next render. */
+typedef enum Wo_Tracer {
+    WO_TRACER_AUTO = 0,
+    WO_TRACER_INTERPRETER = 1,
+    WO_TRACER_JIT = 2,
+    WO_TRACER_LANES = 3,
+} Wo_Tracer;
+void wo_renderer_set_tracer(Wo_Renderer* r, Wo_Tracer tracer);
+/* Compatibility form: 0 = INTERPRETER, anything else = AUTO. */
 void wo_renderer_set_jit(Wo_Renderer* r, int mode);
-/* Which path kernel the last render used: "jit", "interpreter" or "none". */
+/* Which path kernel the last render used: "jit", "lanes", "interpreter" or "none". */
 char const* wo_renderer_trace_path(Wo_Renderer* r);
 
 /* HIP source of the scene-specialised kernel for the current scene (NULL if

@@ -16,9 +16,10 @@
  *                subtrahend first to keep the evaluation stack shallow.)
  *   WO_OP_BOUND  conservative bounding sphere (f[0..2] centre, f[3] R^2,
  *                f[4] R) of the subtree that starts at the next record and
- *                ends at record u0-1.  A kernel MAY skip that subtree (value =
- *                empty set) when no ray of interest can touch the sphere; an
- *                evaluator that ignores BOUND gets identical results.
+ *                ends at record u0-1; u1 = leaves in that subtree.  A kernel MAY
+ *                skip that subtree (value = empty set) when no ray of interest
+ *                can touch the sphere; an evaluator that ignores BOUND (all of
+ *                them, or the small ones) gets identical results.
  *
  * Every record is 32 bytes (8 dwords) so a wave reads one with two 16-byte
  * LDS broadcasts or one scalar s_load_dwordx8.

@@ -69,21 +69,40 @@ def test_ubershader_kats_on_gpu(empty_renderer):
     assert hits == kats["hit_pixels_256_t0"]
 
 
-PATHS = ["jit", "interpreter"]
+PATHS = ["jit", "interpreter", "lanes"]
 
 
 def _scene(name, path="jit", **kw):
     r = wl.Renderer(name, max_nodes=4096)
     info = scenes.build(name, r, **kw) if name in scenes.SCENES else None
-    r.set_jit(1 if path == "jit" else 0)
+    r.set_tracer(path)
     return r, info
 
 
+def _union_only(r):
+    prog, nrec, nprim = r.program()
+    pc = 0
+    while pc < nrec:
+        op = prog[pc].op
+        if op == wl.WO_OP_PRIM:
+            pc += 1 + prog[pc].u0
+            continue
+        if op not in (wl.WO_OP_UNION, wl.WO_OP_BOUND):
+            return False
+        pc += 1
+    return nprim > 0
+
+
 def _check_path(r, path, scene=None):
-    want = path
-    if path == "jit" and scene == "rtiow_cover":
-        want = "interpreter"  # 487 primitives > WOLOLO_JIT_MAX_PRIMS: stays on the interpreter
-    assert r.trace_path() == want, (r.trace_path(), want)
+    """The kernel the tracer setting must have selected (renderer_ext.h Wo_Tracer)."""
+    nprim = r.program()[2]
+    if path == "interpreter":
+        want = "interpreter"
+    elif path == "lanes" and _union_only(r):
+        want = "lanes"
+    else:  # JIT up to WOLOLO_JIT_MAX_PRIMS (256) primitives, e.g. rtiow_cover's 487 stay interpreted
+        want = "jit" if 0 < nprim <= 256 else "interpreter"
+    assert r.trace_path() == want, (scene, r.trace_path(), want)
 
 
 def _oracle_rows(r, params):
@@ -194,7 +213,7 @@ def test_row_tiles_assemble_to_full_frame(nranks, tile, path):
 def test_event_window_overflow_restart(path):
     """A ray crossing > 8 primitive boundaries exercises the window re-collection path."""
     r = wl.Renderer("overflow", max_nodes=256)
-    r.set_jit(1 if path == "jit" else 0)
+    r.set_tracer(path)
     items = []
     for i in range(24):  # a row of overlapping spheres along -z in front of the camera
         s = r.sphere(0.6)
@@ -219,7 +238,7 @@ def test_event_window_overflow_restart(path):
 def test_edge_scenes(path):
     # empty scene: sky only
     r = wl.Renderer("empty", max_nodes=4)
-    r.set_jit(1 if path == "jit" else 0)
+    r.set_tracer(path)
     p = wl.render_params(32, 16, spp=2, mode=wl.MODE_PATHTRACE)
     img = r.render(p)
     ref, segs = _oracle_rows(r, p)
@@ -228,7 +247,7 @@ def test_edge_scenes(path):
     r.close()
     # a lone ground half-space (unbounded), a zero-radius sphere, a degenerate normal
     r = wl.Renderer("edges", max_nodes=16)
-    r.set_jit(1 if path == "jit" else 0)
+    r.set_tracer(path)
     g = r.halfspace((0, 1, 0))
     z = r.sphere(0.0)
     dgn = r.halfspace((0, 0, 0))
@@ -259,3 +278,55 @@ def test_draw_frame_demo_path():
     r.lib.wo_renderer_draw_frame(r.ptr)
     assert wl.last_error() == "" or "draw" not in wl.last_error()
     r.close()
+
+
+def _union_scene(n_spheres=90):
+    """Union-only scene for the lane tracer: overlapping spheres (long event runs, window
+    overflow and BOUND pruning barriers), two boxes (6-plane convex primitives), a ground
+    half-space, glass spheres (bounces that start inside the solid) and metal."""
+    r = wl.Renderer("lanes-union", max_nodes=1024)
+    rng = np.random.default_rng(5)
+    glass, steel, clay = r.dielectric(1.5), r.metal((0.8, 0.8, 0.9), 0.1), r.lambertian((0.6, 0.4, 0.3))
+    items = []
+    for i in range(n_spheres):
+        s = r.sphere(float(rng.uniform(0.2, 0.7)))
+        r.set_material(s, [glass, steel, clay][i % 3])
+        items.append(wl.arg(s, tuple(float(v) for v in (rng.uniform(-3, 3), rng.uniform(0, 2), rng.uniform(-8, 0)))))
+    for cx in (-1.5, 1.5):
+        planes = [r.halfspace(n) for n in ((1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1))]
+        acc = wl.arg(planes[0], (0.5, 0, 0))
+        for h, n in zip(planes[1:], ((-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1))):
+            acc = wl.arg(r.intersection(acc, wl.arg(h, tuple(0.5 * v for v in n))))
+        items.append(wl.arg(acc.node, (cx, 0.6, -2.0)))
+    ground = r.halfspace((0, 1, 0))
+    items.append(wl.arg(ground, (0, -0.2, 0)))
+    while len(items) > 1:
+        nxt = [wl.arg(r.union(items[i], items[i + 1])) for i in range(0, len(items) - 1, 2)]
+        if len(items) % 2:
+            nxt.append(items[-1])
+        items = nxt
+    r.set_camera((0.3, 1.0, 4.0), (0.0, 0.8, -3.0), (0, 1, 0), 50.0)
+    return r
+
+
+@pytest.mark.parametrize("tracer", ["lanes", "auto"])
+def test_lanes_union_scene_bitexact(tracer):
+    r = _union_scene()
+    assert _union_only(r) and r.program()[2] > 64
+    r.set_tracer(tracer)
+    for mode, spp in [(wl.MODE_NORMALS, 1), (wl.MODE_PATHTRACE, 4)]:
+        p = wl.render_params(80, 60, spp=spp, max_depth=8, mode=mode, seed=3)
+        img = r.render(p)
+        assert r.trace_path() == "lanes"
+        ref, _ = _oracle_rows(r, p)
+        _cmp(img, ref, f"union scene mode={mode} tracer={tracer}")
+    r.close()
+
+
+def test_auto_tracer_choices():
+    """AUTO: the RTIOW cover (union-only, 487 primitives) takes the lane tracer; csg32 the JIT."""
+    for name, want in [("rtiow_cover", "lanes"), ("csg32", "jit")]:
+        r, info = _scene(name, "auto")
+        r.render(info.params(width=32, height=18, spp=1))
+        assert r.trace_path() == want, (name, r.trace_path())
+        r.close()

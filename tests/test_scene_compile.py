@@ -145,6 +145,9 @@ def _program_checks(prog, nrec, nprim):
                 depth -= 1
                 k += 1
         assert k == skip and depth == 1
+        # u1 = leaves in the bounded subtree (kernels skip testing small BOUNDs)
+        nleaf = sum(1 for j in range(b + 1, skip) if prog[j].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE))
+        assert prog[b].u1 == nleaf
     return maxsp
 
 

@@ -16,7 +16,7 @@ import os
 import shutil
 import sys
 
-KERNELS = ("wo_jit_pathtrace", "pathtrace_kernel")
+KERNELS = ("wo_jit_pathtrace", "pathtrace_lanes_kernel", "pathtrace_kernel")
 
 
 def _rows(d, pattern):
