@@ -268,10 +268,18 @@ struct InterpTracer {
 // last processed event, exactly as an overflowing window does.  Results are
 // the general algorithm's, bit for bit.
 // ---------------------------------------------------------------------------
+// Compact traversal node: geo = BOUND (centre, R) or sphere primitive (centre,
+// r^2); aux = kind << 30 | value (BOUND: skip target, primitives: ordinal).
+// Generic primitives (half-spaces, several members) read their leaves from the
+// program.  20 bytes per node, staged in LDS when the table fits.
+constexpr uint32_t kNodeBound = 0u, kNodeSphere = 1u, kNodeGeneric = 2u;
+
+template <bool kLds>
 struct LaneTracer {
-    const WoRec* __restrict__ prog;   // full program (hit leaves)
-    const WoRec* __restrict__ trav;   // BOUND / PRIM+leaves, binops dropped
-    const uint32_t* __restrict__ ordpc;
+    const WoRec* __restrict__ prog;      // full program (generic primitives, hit leaves)
+    const float4* geo;                   // LDS or global
+    const uint32_t* aux;
+    const uint32_t* __restrict__ ordpc;  // ordinal -> program pc
     uint32_t ntrav;
 
     __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const { return prog[ordpc[h.ord] + 1u + h.member]; }
@@ -290,54 +298,63 @@ struct LaneTracer {
             uint64_t kcut = kEmptyKey;
             uint32_t pc = 0;
             while (pc < ntrav) {
-                WoRec r = trav[pc];
-                if (r.op == WO_OP_BOUND) {
-                    float ox = r.f[0] - o.x, oy = r.f[1] - o.y, oz = r.f[2] - o.z;
+                const uint32_t a = aux[pc];
+                const float4 g = geo[pc];
+                const uint32_t kind = a >> 30, val = a & 0x3fffffffu;
+                if (kind == kNodeBound) {
+                    float ox = g.x - o.x, oy = g.y - o.y, oz = g.z - o.z;
                     float tca = __builtin_fmaf(oz, d.z, __builtin_fmaf(oy, d.y, ox * d.x));
                     float lx = __builtin_fmaf(-tca, d.x, ox), ly = __builtin_fmaf(-tca, d.y, oy),
                           lz = __builtin_fmaf(-tca, d.z, oz);
                     float d2 = __builtin_fmaf(lz, lz, __builtin_fmaf(ly, ly, lx * lx));
-                    bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, r.f[3])) || (tca + r.f[4] < 0.0f);
+                    bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, g.w * g.w)) || (tca + g.w < 0.0f);
                     // near end of the sphere along the ray, rounded down generously
-                    float lo = (tca - r.f[4]) - 1e-5f * (fabsf(tca) + r.f[4]);
-                    float tnear = __uint_as_float((uint32_t)(win.k[0] >> 32));  // +inf bits pattern when empty
+                    float lo = (tca - g.w) - 1e-5f * (fabsf(tca) + g.w);
+                    float tnear = __uint_as_float((uint32_t)(win.k[0] >> 32));
                     bool prune = !miss && win.k[0] != kEmptyKey && lo > tnear;
                     if (prune) {
                         uint64_t kc = (uint64_t)__float_as_uint(lo) << 32;
                         kcut = kc < kcut ? kc : kcut;
                     }
-                    pc = (miss || prune) ? r.u0 : pc + 1u;
+                    pc = (miss || prune) ? val : pc + 1u;
                 } else {
-                    const uint32_t count = r.u0, ord = r.u1;
                     Ivl iv;
-                    for (uint32_t m = 0; m < count; ++m) {
-                        WoRec L = trav[pc + 1u + m];
+                    if (kind == kNodeSphere) {
                         float la, lb;
-                        if (L.op == WO_LEAF_SPHERE) {
-                            sphere_interval(L.f[0], L.f[1], L.f[2], L.f[3], o, d, la, lb);
-                        } else if (L.u1 != 0u) {
-                            if (!have_inv) {
-                                inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-                                have_inv = true;
+                        sphere_interval(g.x, g.y, g.z, g.w, o, d, la, lb);
+                        ivl_first(iv, la, lb);
+                    } else {
+                        const uint32_t ppc = ordpc[val];
+                        const uint32_t count = prog[ppc].u0;
+                        for (uint32_t m = 0; m < count; ++m) {
+                            WoRec L = prog[ppc + 1u + m];
+                            float la, lb;
+                            if (L.op == WO_LEAF_SPHERE) {
+                                sphere_interval(L.f[0], L.f[1], L.f[2], L.f[3], o, d, la, lb);
+                            } else if (L.u1 != 0u) {
+                                if (!have_inv) {
+                                    inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                                    have_inv = true;
+                                }
+                                uint32_t ax = L.u1 - 1u;
+                                halfspace_axis_interval(ax == 0u ? L.f[0] : (ax == 1u ? L.f[1] : L.f[2]), L.f[3],
+                                                        pick3(o, ax), pick3(d, ax), pick3(inv, ax), la, lb);
+                            } else {
+                                halfspace_interval(L.f[0], L.f[1], L.f[2], L.f[3], o, d, la, lb);
                             }
-                            uint32_t a = L.u1 - 1u;
-                            halfspace_axis_interval(a == 0u ? L.f[0] : (a == 1u ? L.f[1] : L.f[2]), L.f[3],
-                                                    pick3(o, a), pick3(d, a), pick3(inv, a), la, lb);
-                        } else {
-                            halfspace_interval(L.f[0], L.f[1], L.f[2], L.f[3], o, d, la, lb);
+                            if (m == 0u)
+                                ivl_first(iv, la, lb);
+                            else
+                                ivl_meet(iv, la, lb, m);
                         }
-                        if (m == 0u)
-                            ivl_first(iv, la, lb);
-                        else
-                            ivl_meet(iv, la, lb, m);
                     }
                     if (!(iv.a > iv.b)) {
                         if (first && iv.a <= tmin && iv.b > tmin) ++cnt;
-                        uint64_t k0 = event_key(iv.a, ord, 0u, iv.ma), k1 = event_key(iv.b, ord, 1u, iv.mb);
+                        uint64_t k0 = event_key(iv.a, val, 0u, iv.ma), k1 = event_key(iv.b, val, 1u, iv.mb);
                         if (iv.a > tmin && k0 > after) win.insert(k0);
                         if (iv.b > tmin && iv.b < kInf && k1 > after) win.insert(k1);
                     }
-                    pc += 1u + count;
+                    ++pc;
                 }
             }
             if (first) {
@@ -368,18 +385,34 @@ struct LaneTracer {
     }
 };
 
-__global__ __launch_bounds__(kBlock) void pathtrace_lanes_kernel(const WoRec* __restrict__ prog,
-                                                                 const WoRec* __restrict__ trav,
-                                                                 const uint32_t* __restrict__ ordpc,
-                                                                 const WoMaterial* __restrict__ mats, WoFrame fr,
-                                                                 uint32_t ntrav, uint32_t local_rows,
-                                                                 float4* __restrict__ out,
-                                                                 unsigned long long* __restrict__ seg_out) {
-    LaneTracer tr;
+#ifndef WO_LANES_MIN_WAVES
+#define WO_LANES_MIN_WAVES 6
+#endif
+template <bool kLds>
+__global__ __launch_bounds__(kBlock, WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
+    const WoRec* __restrict__ prog, const float4* __restrict__ gnodes, const uint32_t* __restrict__ ordpc,
+    const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t ntrav, uint32_t local_rows, float4* __restrict__ out,
+    unsigned long long* __restrict__ seg_out) {
+    LaneTracer<kLds> tr;
     tr.prog = prog;
-    tr.trav = trav;
     tr.ordpc = ordpc;
     tr.ntrav = ntrav;
+    const uint32_t* gaux = reinterpret_cast<const uint32_t*>(gnodes + ntrav);
+    if constexpr (kLds) {
+        extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+        float4* lgeo = reinterpret_cast<float4*>(smem);
+        uint32_t* laux = smem + ntrav * 4u;
+        for (uint32_t i = threadIdx.x; i < ntrav; i += kBlock) {
+            lgeo[i] = gnodes[i];
+            laux[i] = gaux[i];
+        }
+        __syncthreads();
+        tr.geo = lgeo;
+        tr.aux = laux;
+    } else {
+        tr.geo = gnodes;
+        tr.aux = gaux;
+    }
     pathtrace_block(tr, mats, fr, local_rows, out, seg_out);
 }
 
@@ -494,8 +527,8 @@ struct WoDev {
     float4* d_frame;
     size_t frame_cap;
     hipStream_t stream;
-    // lane traversal (union-only programs): program without binops + ordinal -> pc
-    WoRec* d_trav;
+    // lane traversal (union-only programs): compact nodes [geo float4 x n][aux u32 x n] + ordinal -> pc
+    float4* d_trav;
     size_t trav_cap;
     uint32_t* d_ordpc;
     size_t ordpc_cap;
@@ -601,37 +634,67 @@ static int build_trav(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
         }
     }
     if (!union_only) return 0;
-    std::vector<WoRec> trav;
+    // pass 1: node index of every program record (binops and leaves map to the next node)
     std::vector<uint32_t> map(n_recs + 1u, 0u), ordpc(n_prims, 0u);
-    trav.reserve(n_recs);
+    uint32_t nn = 0;
     for (uint32_t pc = 0; pc < n_recs;) {
+        map[pc] = nn;
         const WoRec& r = prog[pc];
-        map[pc] = (uint32_t)trav.size();
         if (r.op == WO_OP_PRIM) {
             if (r.u1 < n_prims) ordpc[r.u1] = pc;
-            for (uint32_t m = 0; m <= r.u0; ++m) {
-                if (m) map[pc + m] = (uint32_t)trav.size();
-                trav.push_back(prog[pc + m]);
-            }
+            for (uint32_t m = 1; m <= r.u0; ++m) map[pc + m] = nn + 1u;
+            ++nn;
             pc += 1u + r.u0;
         } else {
-            if (r.op == WO_OP_BOUND) trav.push_back(r);
+            if (r.op == WO_OP_BOUND) ++nn;
             ++pc;
         }
     }
-    map[n_recs] = (uint32_t)trav.size();
-    for (WoRec& r : trav)
-        if (r.op == WO_OP_BOUND) r.u0 = r.u0 <= n_recs ? map[r.u0] : (uint32_t)trav.size();
-    if (ensure_buffer(&dev->d_trav, &dev->trav_cap, trav.size() * sizeof(WoRec), err, errlen)) return -1;
+    map[n_recs] = nn;
+    if (nn >= (1u << 30) || n_prims >= (1u << 30)) {
+        snprintf(err, errlen, "traversal table too large");
+        return -1;
+    }
+    // pass 2: geo (float4) then aux (u32), one buffer
+    std::vector<float4> geo(nn);
+    std::vector<uint32_t> aux(nn);
+    uint32_t k = 0;
+    for (uint32_t pc = 0; pc < n_recs;) {
+        const WoRec& r = prog[pc];
+        if (r.op == WO_OP_PRIM) {
+            const WoRec& L = prog[pc + 1u];
+            if (r.u0 == 1u && L.op == WO_LEAF_SPHERE) {
+                geo[k] = make_float4(L.f[0], L.f[1], L.f[2], L.f[3]);
+                aux[k] = (kNodeSphere << 30) | r.u1;
+            } else {
+                geo[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                aux[k] = (kNodeGeneric << 30) | r.u1;
+            }
+            ++k;
+            pc += 1u + r.u0;
+        } else {
+            if (r.op == WO_OP_BOUND) {
+                geo[k] = make_float4(r.f[0], r.f[1], r.f[2], r.f[4]);
+                aux[k] = (kNodeBound << 30) | (r.u0 <= n_recs ? map[r.u0] : nn);
+                ++k;
+            }
+            ++pc;
+        }
+    }
+    size_t bytes = (size_t)nn * (sizeof(float4) + sizeof(uint32_t));
+    if (ensure_buffer(&dev->d_trav, &dev->trav_cap, bytes, err, errlen)) return -1;
     if (ensure_buffer(&dev->d_ordpc, &dev->ordpc_cap, (size_t)n_prims * sizeof(uint32_t), err, errlen)) return -1;
-    hipError_t e = hipMemcpy(dev->d_trav, trav.data(), trav.size() * sizeof(WoRec), hipMemcpyHostToDevice);
+    hipError_t e = hipMemcpy(dev->d_trav, geo.data(), (size_t)nn * sizeof(float4), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy((char*)dev->d_trav + (size_t)nn * sizeof(float4), aux.data(), (size_t)nn * sizeof(uint32_t),
+                      hipMemcpyHostToDevice);
     if (e == hipSuccess)
         e = hipMemcpy(dev->d_ordpc, ordpc.data(), (size_t)n_prims * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         set_err(err, errlen, "hipMemcpy(traversal table)", e);
         return -1;
     }
-    dev->n_trav = (uint32_t)trav.size();
+    dev->n_trav = nn;
     dev->union_only = true;
     return 0;
 }
@@ -791,6 +854,9 @@ extern "C" void wo_dev_set_lanes(WoDev* dev, int on) {
 extern "C" double wo_dev_jit_compile_sec(WoDev* dev) { return dev ? dev->jit_compile_sec : 0.0; }
 
 static const size_t kLdsBudget = 64u * 1024u;
+// Lane-traversal nodes in LDS: up to ~1200 nodes keeps 6 workgroups per CU
+// (24 KB + 7 KB of sample accumulators each).
+static const size_t kLanesLdsBudget = 24u * 1024u;
 
 extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, void* stream_v,
                              unsigned long long* d_segments, char* err, size_t errlen) {
@@ -823,8 +889,15 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
         }
         dim3 grid((fr.width + kPtTile - 1) / kPtTile, (local_rows + kPtTile - 1) / kPtTile);
         if (dev->lanes_on && dev->union_only && !dev->jit_fn) {
-            hipLaunchKernelGGL(pathtrace_lanes_kernel, grid, dim3(kBlock), 0, stream, dev->d_prog, dev->d_trav,
-                               dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, d_segments);
+            size_t lds = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
+            if (lds <= kLanesLdsBudget)
+                hipLaunchKernelGGL(pathtrace_lanes_kernel<true>, grid, dim3(kBlock), lds, stream, dev->d_prog,
+                                   dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out,
+                                   d_segments);
+            else
+                hipLaunchKernelGGL(pathtrace_lanes_kernel<false>, grid, dim3(kBlock), 0, stream, dev->d_prog,
+                                   dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out,
+                                   d_segments);
         } else if (dev->jit_fn) {
             const WoRec* p = dev->d_prog;
             const WoMaterial* m = dev->d_mats;
