@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--depth", type=int, default=8)
-    ap.add_argument("--tile-rows", type=int, default=16)
+    ap.add_argument("--tile-rows", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tracer", default=os.environ.get("WOLOLO_TRACER", "auto"),

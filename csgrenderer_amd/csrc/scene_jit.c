@@ -308,10 +308,10 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "#define WO_JIT_MIN_WAVES 6\n#endif\n"
          "extern \"C\" __global__ __launch_bounds__(256, WO_JIT_MIN_WAVES) void wo_jit_pathtrace(\n"
          "    const WoRec* __restrict__ prog, const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t local_rows,\n"
-         "    float4* __restrict__ out, unsigned long long* __restrict__ seg_out) {\n"
+         "    float4* __restrict__ out, unsigned long long* __restrict__ seg_slots) {\n"
          "  JitTracer tr;\n"
          "  tr.prog = prog;\n"
-         "  wodev::pathtrace_block(tr, mats, fr, local_rows, out, seg_out);\n"
+         "  wodev::pathtrace_block(tr, mats, fr, local_rows, out, seg_slots);\n"
          "}\n");
     if (g.err || b.oom) {
         free(b.s);

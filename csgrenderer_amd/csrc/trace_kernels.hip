@@ -392,7 +392,7 @@ template <bool kLds>
 __global__ __launch_bounds__(kBlock, WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
     const WoRec* __restrict__ prog, const float4* __restrict__ gnodes, const uint32_t* __restrict__ ordpc,
     const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t ntrav, uint32_t local_rows, float4* __restrict__ out,
-    unsigned long long* __restrict__ seg_out) {
+    unsigned long long* __restrict__ seg_slots) {
     LaneTracer<kLds> tr;
     tr.prog = prog;
     tr.ordpc = ordpc;
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(kBlock, WO_LANES_MIN_WAVES) void pathtrace_lanes_ke
         tr.geo = gnodes;
         tr.aux = gaux;
     }
-    pathtrace_block(tr, mats, fr, local_rows, out, seg_out);
+    pathtrace_block(tr, mats, fr, local_rows, out, seg_slots);
 }
 
 // ---------------------------------------------------------------------------
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(kBlock) void pathtrace_kernel(const WoRec* __restri
                                                            const WoMaterial* __restrict__ mats, WoFrame fr,
                                                            KLayout lay, uint32_t local_rows,
                                                            float4* __restrict__ out,
-                                                           unsigned long long* __restrict__ seg_out) {
+                                                           unsigned long long* __restrict__ seg_slots) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t nrec = fr.n_recs;
@@ -495,7 +495,26 @@ __global__ __launch_bounds__(kBlock) void pathtrace_kernel(const WoRec* __restri
     tr.ordpc = ws + lay.ordpc_off;
     tr.hib = ws + lay.hib_off;
     tr.lane = lane;
-    pathtrace_block(tr, mats, fr, local_rows, out, seg_out);
+    pathtrace_block(tr, mats, fr, local_rows, out, seg_slots);
+}
+
+// Sums (and clears) the segment slots into the caller's counter.
+__global__ __launch_bounds__(kBlock) void seg_collect_kernel(unsigned long long* __restrict__ slots,
+                                                             unsigned long long* __restrict__ counter) {
+    __shared__ unsigned long long part[kBlock / 64];
+    unsigned long long v = 0;
+    for (uint32_t i = threadIdx.x; i < kSegSlots; i += kBlock) {
+        v += slots[i * kSegStride];
+        slots[i * kSegStride] = 0ull;
+    }
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((threadIdx.x & 63u) == 0u) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0u) {
+        unsigned long long t = 0;
+        for (uint32_t w = 0; w < kBlock / 64u; ++w) t += part[w];
+        if (t) atomicAdd(counter, t);
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void assemble_kernel(const float4* __restrict__ gathered, float4* __restrict__ frame,
@@ -533,6 +552,7 @@ struct WoDev {
     uint32_t* d_ordpc;
     size_t ordpc_cap;
     uint32_t n_trav;
+    unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
     bool union_only;
     bool lanes_on;
     // scene-specialised kernel (hiprtc)
@@ -596,6 +616,7 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
     if (dev->d_frame) (void)hipFree(dev->d_frame);
     if (dev->d_trav) (void)hipFree(dev->d_trav);
     if (dev->d_ordpc) (void)hipFree(dev->d_ordpc);
+    if (dev->d_segslots) (void)hipFree(dev->d_segslots);
     if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
     (void)hipStreamDestroy(dev->stream);
     delete dev;
@@ -887,21 +908,41 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
             snprintf(err, errlen, "scene has %u primitives (max %u)", fr.n_prims, (1u << 20) - 1u);
             return -1;
         }
-        dim3 grid((fr.width + kPtTile - 1) / kPtTile, (local_rows + kPtTile - 1) / kPtTile);
+        dim3 grid((fr.width + kTileW - 1) / kTileW, (local_rows + kTileH - 1) / kTileH);
+        if (grid.y > 65535u) {
+            snprintf(err, errlen, "frame too tall (%u local rows)", local_rows);
+            return -1;
+        }
+        // the kernels count segments into the per-device slots; seg_collect_kernel
+        // then moves the sum into the caller's counter
+        unsigned long long* slots = nullptr;
+        if (d_segments) {
+            if (!dev->d_segslots) {
+                e = hipMalloc((void**)&dev->d_segslots, kSegSlots * kSegStride * sizeof(unsigned long long));
+                if (e == hipSuccess)
+                    e = hipMemset(dev->d_segslots, 0, kSegSlots * kSegStride * sizeof(unsigned long long));
+                if (e != hipSuccess) {
+                    dev->d_segslots = nullptr;
+                    set_err(err, errlen, "hipMalloc(segment slots)", e);
+                    return -1;
+                }
+            }
+            slots = dev->d_segslots;
+        }
         if (dev->lanes_on && dev->union_only && !dev->jit_fn) {
             size_t lds = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
             if (lds <= kLanesLdsBudget)
                 hipLaunchKernelGGL(pathtrace_lanes_kernel<true>, grid, dim3(kBlock), lds, stream, dev->d_prog,
                                    dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out,
-                                   d_segments);
+                                   slots);
             else
                 hipLaunchKernelGGL(pathtrace_lanes_kernel<false>, grid, dim3(kBlock), 0, stream, dev->d_prog,
                                    dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out,
-                                   d_segments);
+                                   slots);
         } else if (dev->jit_fn) {
             const WoRec* p = dev->d_prog;
             const WoMaterial* m = dev->d_mats;
-            unsigned long long* s = d_segments;
+            unsigned long long* s = slots;
             void* args[] = {&p, &m, &fr, &local_rows, &out, &s};
             e = hipModuleLaunchKernel(dev->jit_fn, grid.x, grid.y, 1, kBlock, 1, 1, 0, stream, args, nullptr);
             if (e != hipSuccess) {
@@ -919,15 +960,16 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
             size_t prog_bytes = (size_t)fr.n_recs * sizeof(WoRec);
             if (prog_bytes + scratch <= kLdsBudget) {
                 hipLaunchKernelGGL(pathtrace_kernel<true>, grid, dim3(kBlock), prog_bytes + scratch, stream,
-                                   dev->d_prog, dev->d_mats, fr, lay, local_rows, out, d_segments);
+                                   dev->d_prog, dev->d_mats, fr, lay, local_rows, out, slots);
             } else if (scratch <= kLdsBudget) {
                 hipLaunchKernelGGL(pathtrace_kernel<false>, grid, dim3(kBlock), scratch, stream, dev->d_prog,
-                                   dev->d_mats, fr, lay, local_rows, out, d_segments);
+                                   dev->d_mats, fr, lay, local_rows, out, slots);
             } else {
                 snprintf(err, errlen, "scene too large for the LDS scratch (%zu bytes per workgroup)", scratch);
                 return -1;
             }
         }
+        if (slots) hipLaunchKernelGGL(seg_collect_kernel, dim3(1), dim3(kBlock), 0, stream, slots, d_segments);
     } else {
         snprintf(err, errlen, "unknown shading mode %u", fr.mode);
         return -1;
