@@ -98,7 +98,9 @@ def main():
     r.set_tracer("interpreter" if args.jit == 0 else args.tracer)
     W, H, T = params.width, params.height, args.tile_rows
     lr = wl.local_rows(H, T, world)
-    out = torch.empty((lr, W, 4), dtype=torch.float32, device=dev)
+    pipelined = world > 1 and not gloo
+    # two render buffers when pipelined: frame k+1 renders while frame k is gathered
+    outs = [torch.empty((lr, W, 4), dtype=torch.float32, device=dev) for _ in range(2 if pipelined else 1)]
     seg = torch.zeros(1, dtype=torch.int64, device=dev)
     stacked = gathered = frame = None
     if world > 1 and rank == 0:
@@ -106,25 +108,40 @@ def main():
         stacked = torch.empty((world, lr, W, 4), dtype=torch.float32, device="cpu" if gloo else dev)
         gathered = list(stacked.unbind(0))
         frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sh = stream.cuda_stream
+    cs = torch.cuda.current_stream(dev)  # gather + assemble (RCCL's stream follows it)
+    rs = torch.cuda.Stream(dev) if pipelined else cs  # render
     k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     k_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    rendered = [torch.cuda.Event() for _ in outs]
+    released = [None for _ in outs]  # gather of the frame that last used the buffer
+    frame_no = [0]
 
     def step(i=None):
+        b = frame_no[0] % len(outs)
+        frame_no[0] += 1
+        out = outs[b]
+        if released[b] is not None:
+            rs.wait_event(released[b])
         if i is not None:
-            k_start[i].record(stream)
-        r.render_rows_device(params, out.data_ptr(), T, rank, world, sh, seg.data_ptr())
+            k_start[i].record(rs)
+        r.render_rows_device(params, out.data_ptr(), T, rank, world, rs.cuda_stream, seg.data_ptr())
         if i is not None:
-            k_end[i].record(stream)
+            k_end[i].record(rs)
         if world > 1:
+            if pipelined:
+                rendered[b].record(rs)
+                cs.wait_event(rendered[b])
             src = out.cpu() if gloo else out
             if rank == 0:
                 dist.gather(src, gather_list=gathered, dst=0)
                 g = stacked.to(dev, non_blocking=False) if gloo else stacked
-                wl.assemble_rows_device(g.data_ptr(), frame.data_ptr(), W, H, T, world, sh)
+                wl.assemble_rows_device(g.data_ptr(), frame.data_ptr(), W, H, T, world, cs.cuda_stream)
             else:
                 dist.gather(src, dst=0)
+            if pipelined:
+                ev = torch.cuda.Event()
+                ev.record(cs)
+                released[b] = ev
 
     for _ in range(args.warmup):
         step()
@@ -155,7 +172,7 @@ def main():
     if args.verify and rank == 0:
         import numpy as np
         full = r.render(params)
-        got = (frame if world > 1 else out[:H]).cpu().numpy()
+        got = (frame if world > 1 else outs[(frame_no[0] - 1) % len(outs)][:H]).cpu().numpy()
         verified = bool(np.array_equal(got, full))
         if not verified:
             bad = int((got != full).any(axis=-1).sum())
@@ -211,7 +228,8 @@ def main():
                                    f"{info.spheres} spheres + {info.halfspaces} half-spaces, {info.binops} binops",
                        "scene": info.name, "width": W, "height": H, "spp": params.spp,
                        "max_depth": params.max_depth, "tile_rows": T,
-                       "parallelism": f"row-cyclic tiles x{world}" + (f" + {'gloo (host-staged)' if gloo else 'RCCL'} gather" if world > 1 else "")},
+                       "parallelism": f"row-cyclic tiles x{world}" + (f" + {'gloo (host-staged)' if gloo else 'RCCL'} gather" if world > 1 else "")
+                                      + (" overlapped with the next frame's render" if pipelined else "")},
             "fps": round(steps / elapsed_s, 3),
             "msamples_per_s": round(samples * steps / elapsed_s / 1e6, 3),
             "segments_per_frame": segs_all // steps,
