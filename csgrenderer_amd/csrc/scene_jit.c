@@ -303,9 +303,14 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "  }\n"
              "};\n");
     }
+    /* Waves per SIMD the register budget is sized for (measured, 1920x1080x64):
+     * csg32 (18 primitives) 6.62 ms at 6, 6.50 at 7, 6.65 at 8; csg256 balanced /
+     * chain (128) 23.7 / 38.0 ms at 6, 21.3 / 33.8 at 8. */
     bput(&b,
-         "\n#ifndef WO_JIT_MIN_WAVES  // 6 waves/SIMD: <= 80 VGPRs, no spills (csg32: 9.87 vs 10.0 ms at 5)\n"
-         "#define WO_JIT_MIN_WAVES 6\n#endif\n"
+         "\n#ifndef WO_JIT_MIN_WAVES\n"
+         "#define WO_JIT_MIN_WAVES %u\n#endif\n",
+         n_prims > 64u ? 8u : 7u);
+    bput(&b,
          "extern \"C\" __global__ __launch_bounds__(256, WO_JIT_MIN_WAVES) void wo_jit_pathtrace(\n"
          "    const WoRec* __restrict__ prog, const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t local_rows,\n"
          "    float4* __restrict__ out, unsigned long long* __restrict__ seg_slots) {\n"

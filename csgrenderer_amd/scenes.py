@@ -201,7 +201,7 @@ def _overlapping_pairs(r: Renderer, rng: Pcg32, n_pairs: int, lo, hi, rmin: floa
     return items
 
 
-def build_csg32(r: Renderer, seed: int = 32, width=1920, height=1080, spp=64) -> SceneInfo:
+def build_csg32(r: Renderer, seed: int = 32, width=1920, height=1080, spp=64, union_only=False) -> SceneInfo:
     """C3: 32 leaves (20 spheres + 12 half-spaces), 31 binops, 63 nodes.
 
     Box A is a 12 x 0.5 x 12 floor slab (y in [-0.5, 0]) minus sphere0 (a crater);
@@ -221,14 +221,15 @@ def build_csg32(r: Renderer, seed: int = 32, width=1920, height=1080, spp=64) ->
     s0, s1 = r.sphere(1.2), r.sphere(1.0)
     r.set_material(s0, r.lambertian((0.7, 0.3, 0.2)))
     r.set_material(s1, r.metal((0.9, 0.8, 0.5), 0.1))
-    crater = r.difference(arg(slab), arg(s0, (2.5, 0.3, 1.5)))
+    crater = (r.union if union_only else r.difference)(arg(slab), arg(s0, (2.5, 0.3, 1.5)))
     rounded = r.intersection(arg(cube), arg(s1, (-2.0, 0.75, 0.0)))
-    pairs = _overlapping_pairs(r, rng, 9, (-4.0, 0.5, -4.0), (4.0, 2.0, 4.0), 0.3, 0.8, _cycle("udi"))
+    pairs = _overlapping_pairs(r, rng, 9, (-4.0, 0.5, -4.0), (4.0, 2.0, 4.0), 0.3, 0.8,
+                               _cycle("uui" if union_only else "udi"))
     rest, roff = _balanced(r, pairs, _cycle("u"))
     objs = r.union(arg(crater), arg(rounded))
     r.union(arg(objs), arg(rest, roff))
     r.set_camera((0.0, 4.5, 10.0), (0.0, 0.6, 0.0), (0, 1, 0), 45.0, 0.0, 10.0)
-    return SceneInfo("csg32", spheres=20, halfspaces=12, binops=31, width=width, height=height, spp=spp,
+    return SceneInfo("csg32_union" if union_only else "csg32", spheres=20, halfspaces=12, binops=31, width=width, height=height, spp=spp,
                      max_depth=8)
 
 
@@ -272,6 +273,9 @@ def build_csg256(r: Renderer, seed: int = 256, shape: str = "balanced", width=19
 SCENES = {
     "rtiow_cover": build_rtiow_cover,
     "csg32": build_csg32,
+    # csg32's geometry with the differences made unions (an A/B scene for the
+    # union-only lane tracer; not a BASELINE config)
+    "csg32_union": lambda r, **k: build_csg32(r, union_only=True, **k),
     "csg256_balanced": lambda r, **k: build_csg256(r, shape="balanced", **k),
     "csg256_chain": lambda r, **k: build_csg256(r, shape="chain", **k),
 }

@@ -16,7 +16,8 @@ from ctypes import (POINTER, Structure, c_bool, c_char_p, c_double, c_float, c_i
                     c_ulonglong, c_void_p)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libwololo.so")
+# WOLOLO_LIB: another build of the same library (A/B measurements of build options)
+LIB_PATH = os.environ.get("WOLOLO_LIB") or os.path.join(PKG_DIR, "lib", "libwololo.so")
 
 # ---- wo_scene.h constants -------------------------------------------------------------------
 WO_OP_PRIM, WO_OP_UNION, WO_OP_INTER, WO_OP_DIFF, WO_OP_RDIFF, WO_OP_BOUND = 1, 2, 3, 4, 5, 6
