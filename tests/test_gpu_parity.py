@@ -330,3 +330,21 @@ def test_auto_tracer_choices():
         r.render(info.params(width=32, height=18, spp=1))
         assert r.trace_path() == want, (name, r.trace_path())
         r.close()
+
+
+@pytest.mark.parametrize("window", ["lds2", "lds8", "registers"])
+def test_jit_event_windows(window, monkeypatch):
+    """The specialised kernel's two event windows (LDS list, register window) and
+    the LDS list's overflow barrier (capacity 2 forces it on most rays that meet
+    more than one primitive) all give the oracle's frame."""
+    monkeypatch.setenv("WOLOLO_JIT_LDS_EVENTS", "0" if window == "registers" else "1")
+    if window == "lds2":
+        monkeypatch.setenv("WOLOLO_JIT_FLAGS", "-DWO_LDS_EVENTS=2")
+    for name in ["csg32", "csg256_chain"]:
+        r, info = _scene(name, "jit")
+        p = info.params(width=64, height=36, spp=4, seed=11)
+        img = r.render(p)
+        _check_path(r, "jit")
+        ref, _ = _oracle_rows(r, p)
+        _cmp(img, ref, f"{name} window={window}")
+        r.close()
