@@ -84,6 +84,7 @@ typedef struct Gen {
     int lds_events;            /* event window: LDS list (LdsWindow) or registers (Window) */
     Buf* b;
     uint32_t nbound;  /* BOUND counter (cull flag names) */
+    int first_pass;   /* gen_collect: the first pass (cull tests, bits at t_min) or a re-collect */
     uint32_t nval;    /* value counter (eval temporaries) */
     int err;
 } Gen;
@@ -100,12 +101,14 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
             uint32_t vb[5];
             for (int i = 0; i < 5; ++i) vb[i] = fbits(r->f[i]);
             uint32_t k = g->nbound++;
-            bput(g->b, "%*sif (first) {  // BOUND %u\n", indent, "", k);
-            emit_consts(g->b, indent + 2, "float", nb, vb, 5);
-            bput(g->b,
-                 "%*s  if (__ballot(wodev::bound_may_hit(bc0, bc1, bc2, bc3, bc4, o, d)) == 0ull) cull[%u] |= %uu;\n"
-                 "%*s}\n",
-                 indent, "", k / 32, 1u << (k % 32), indent, "");
+            if (g->first_pass) { /* the wave's cull decision; re-collects reuse it */
+                bput(g->b, "%*s{  // BOUND %u\n", indent, "", k);
+                emit_consts(g->b, indent + 2, "float", nb, vb, 5);
+                bput(g->b,
+                     "%*s  if (__ballot(wodev::bound_may_hit(bc0, bc1, bc2, bc3, bc4, o, d)) == 0ull) cull[%u] |= %uu;\n"
+                     "%*s}\n",
+                     indent, "", k / 32, 1u << (k % 32), indent, "");
+            }
             bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
             gen_collect(g, pc + 1, r->u0, indent + 2);
             bput(g->b, "%*s}\n", indent, "");
@@ -145,14 +148,22 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
             uint32_t vk[2] = {ord << 12, (ord << 12) | (1u << 11)};
             bput(g->b, "%*s  if (!(iv.a > iv.b)) {\n", indent, "");
             emit_consts(g->b, indent + 4, "uint32_t", nk, vk, 2);
-            /* one lane branch per event: the key test against `after` (re-collect) folded in */
-            bput(g->b,
-                 "%*s    if (first) bits[%u] |= ((iv.a <= tmin && iv.b > tmin) ? 1u : 0u) << %u;\n"
-                 "%*s    uint64_t k0 = wodev::event_key_lo(iv.a, ka | iv.ma), k1 = wodev::event_key_lo(iv.b, kb | iv.mb);\n"
-                 "%*s    if ((iv.a > tmin) & (k0 > after)) win.insert(k0);\n"
-                 "%*s    if ((iv.b > tmin) & (iv.b < wodev::kInf) & (k1 > after)) win.insert(k1);\n"
-                 "%*s  }\n%*s}\n",
-                 indent, "", ord / 32, ord % 32, indent, "", indent, "", indent, "", indent, "", indent, "");
+            /* one lane branch per event.  The first pass also sets the membership
+             * bit at t_min; a re-collect keeps only the events after `after`. */
+            if (g->first_pass)
+                bput(g->b,
+                     "%*s    bits[%u] |= ((iv.a <= tmin && iv.b > tmin) ? 1u : 0u) << %u;\n"
+                     "%*s    if (iv.a > tmin) win.insert(wodev::event_key_lo(iv.a, ka | iv.ma));\n"
+                     "%*s    if ((iv.b > tmin) & (iv.b < wodev::kInf)) win.insert(wodev::event_key_lo(iv.b, kb | iv.mb));\n"
+                     "%*s  }\n%*s}\n",
+                     indent, "", ord / 32, ord % 32, indent, "", indent, "", indent, "", indent, "");
+            else
+                bput(g->b,
+                     "%*s    uint64_t k0 = wodev::event_key_lo(iv.a, ka | iv.ma), k1 = wodev::event_key_lo(iv.b, kb | iv.mb);\n"
+                     "%*s    if ((iv.a > tmin) & (k0 > after)) win.insert(k0);\n"
+                     "%*s    if ((iv.b > tmin) & (iv.b < wodev::kInf) & (k1 > after)) win.insert(k1);\n"
+                     "%*s  }\n%*s}\n",
+                     indent, "", indent, "", indent, "", indent, "", indent, "");
             pc += 1 + cnt;
         } else {
             ++pc; /* binops: nothing to collect */
@@ -301,21 +312,24 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         uint32_t ncw = nbounds ? (nbounds + 31u) / 32u : 1u;
         bput(&b, "    uint32_t cull[%u];  // bit k: BOUND k culled for this wave\n", ncw);
         for (uint32_t w = 0; w < ncw; ++w) bput(&b, "    cull[%u] = 0u;\n", w);
+        /* First pass (culls, membership at t_min, every event), then the sweep;
+         * the re-collect copy (events after the last processed one, when the
+         * window had dropped some) is separate code so the common pass carries
+         * none of its tests. */
         bput(&b,
              "    %s win; %swin.clear();\n"
-             "    bool collect = true, first = true, have = false;\n"
              "    uint64_t after = 0ull, key = 0ull;\n"
-             "    uint32_t root = 0u;\n"
-             "    for (;;) {\n"
-             "      if (collect) {\n",
+             "    {\n",
              g.lds_events ? "wodev::LdsWindow" : "wodev::Window", g.lds_events ? "win.ev = ev; " : "");
         g.nbound = 0;
-        gen_collect(&g, 0, n_recs, 8);
+        g.first_pass = 1;
+        gen_collect(&g, 0, n_recs, 6);
         bput(&b,
-             "        collect = false;\n"
-             "        if (first && win.empty()) return false;\n"
-             "        first = false;\n"
-             "      }\n"
+             "    }\n"
+             "    if (win.empty()) return false;\n"
+             "    bool have = false;\n"
+             "    uint32_t root = 0u;\n"
+             "    for (;;) {\n"
              "      uint32_t r;\n"
              "      {\n");
         g.nbound = 0;
@@ -326,8 +340,15 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "      root = r;\n"
              "      if (!win.next(key)) {  // key keeps the last processed event\n"
              "        if (!win.dropped()) return false;\n"
-             "        after = key; win.clear(); collect = true; have = false;\n"
-             "        continue;\n"
+             "        after = key;\n"
+             "        win.clear();\n"
+             "        {\n");
+        g.nbound = 0;
+        g.first_pass = 0;
+        gen_collect(&g, 0, n_recs, 10);
+        bput(&b,
+             "        }\n"
+             "        if (!win.next(key)) return false;\n"
              "      }\n"
              "      have = true;\n"
              "      {\n"
