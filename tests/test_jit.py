@@ -15,13 +15,14 @@ def test_csg32_source_compiles_for_gfx950(hostonly):
     prog, nrec, nprim = r.program()
     src = r.jit_source()
     assert src is not None
-    # one intersection call per leaf, one cull flag per BOUND, ordinal table of every primitive
+    # one intersection call per leaf in each of the two collect passes (first pass,
+    # re-collect), one cull flag per BOUND, ordinal table of every primitive
     nleaf = sum(1 for i in range(nrec) if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE))
-    assert len(re.findall(r"wodev::(sphere|halfspace|halfspace_axis)_interval\(", src)) == nleaf
+    assert len(re.findall(r"wodev::(sphere|halfspace|halfspace_axis)_interval\(", src)) == 2 * nleaf
     # the slab and the cube are axis-aligned: tagged by the compiler, emitted on the fast path
     naxis = sum(1 for i in range(nrec) if prog[i].op == wl.WO_LEAF_HALFSPACE and prog[i].u1 != 0)
     assert naxis >= 12
-    assert len(re.findall(r"wodev::halfspace_axis_interval\(", src)) == naxis
+    assert len(re.findall(r"wodev::halfspace_axis_interval\(", src)) == 2 * naxis
     # wave-level tests only for BOUND subtrees of >= 8 leaves (scene_jit.c, WOLOLO_JIT_BOUND_MIN_LEAVES)
     nb = sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND and prog[i].u1 >= 8)
     assert 0 < nb < sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND)
