@@ -282,8 +282,21 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     for (uint32_t i = 0; i < n_recs; ++i) nbounds += prog[i].op == WO_OP_BOUND && prog[i].u1 >= g.bound_min_leaves;
 
     bput(&b, "// generated by scene_jit.c: %u records, %u primitives, %u bounds\n", n_recs, n_prims, nbounds);
-    bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n\n", g.lds_events,
-         tree_depth(prog, n_recs));
+    /* Small programs are copied to LDS per workgroup with the materials they use:
+     * the hit leaf / material reads then cost an LDS round trip instead of
+     * dependent global loads.  Larger ones stay in global memory, where the LDS
+     * would cost occupancy. */
+    uint32_t n_mats_used = 1;
+    for (uint32_t i = 0; i < n_recs; ++i)
+        if ((prog[i].op == WO_LEAF_SPHERE || prog[i].op == WO_LEAF_HALFSPACE) && prog[i].u0 + 1u > n_mats_used)
+            n_mats_used = prog[i].u0 + 1u;
+    int lds_prog = (size_t)n_recs * sizeof(WoRec) + (size_t)n_mats_used * sizeof(WoMaterial) + 4u * n_prims <= 6144u;
+    {
+        const char* v = getenv("WOLOLO_JIT_LDS_PROG");
+        if (v && *v) lds_prog = v[0] != '0';
+    }
+    bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
+         g.lds_events, tree_depth(prog, n_recs), lds_prog);
     bput(&b, "__constant__ uint32_t kOrdPc[%u] = {", n_prims ? n_prims : 1u);
     if (!n_prims) bput(&b, "0u");
     for (uint32_t i = 0, o = 0; i < n_recs; ++i)
@@ -292,9 +305,10 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     bput(&b,
          "struct JitTracer {\n"
          "  const WoRec* __restrict__ prog;\n"
+         "  const uint32_t* __restrict__ ordpc;\n"
          "  uint64_t* ev;  // LDS event list column (LdsWindow)\n"
          "  __device__ __forceinline__ WoRec hit_leaf(const wodev::Hit& h) const {\n"
-         "    return prog[kOrdPc[h.ord] + 1u + h.member];\n"
+         "    return prog[ordpc[h.ord] + 1u + h.member];\n"
          "  }\n"
          "  __device__ __forceinline__ bool trace(wodev::F3 o, wodev::F3 d, wodev::Hit& hit) {\n");
     if (n_prims == 0) {
@@ -373,15 +387,32 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "    const WoRec* __restrict__ prog, const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t local_rows,\n"
          "    float4* __restrict__ out, unsigned long long* __restrict__ seg_slots) {\n"
          "  JitTracer tr;\n"
-         "  tr.prog = prog;\n"
          "#if WO_JIT_LDS_EVENTS\n"
          "  __shared__ uint64_t s_ev[wodev::kLdsEvents * wodev::kBlock];\n"
          "  tr.ev = s_ev + threadIdx.x;\n"
          "#else\n"
          "  tr.ev = nullptr;\n"
          "#endif\n"
-         "  wodev::pathtrace_block(tr, mats, fr, local_rows, out, seg_slots);\n"
-         "}\n");
+         "#if WO_JIT_LDS_PROG  // hit-leaf and material reads from LDS (pathtrace_block's first barrier orders the copy)\n"
+         "  __shared__ WoRec s_prog[%u];\n"
+         "  __shared__ WoMaterial s_mats[%u];\n"
+         "  __shared__ uint32_t s_ordpc[%u];\n"
+         "  for (uint32_t i = threadIdx.x; i < %uu; i += wodev::kBlock)\n"
+         "    reinterpret_cast<uint32_t*>(s_prog)[i] = reinterpret_cast<const uint32_t*>(prog)[i];\n"
+         "  for (uint32_t i = threadIdx.x; i < %uu; i += wodev::kBlock)\n"
+         "    reinterpret_cast<uint32_t*>(s_mats)[i] = reinterpret_cast<const uint32_t*>(mats)[i];\n"
+         "  for (uint32_t i = threadIdx.x; i < %uu; i += wodev::kBlock) s_ordpc[i] = kOrdPc[i];\n"
+         "  tr.prog = s_prog;\n"
+         "  tr.ordpc = s_ordpc;\n"
+         "  const WoMaterial* m = s_mats;\n"
+         "#else\n"
+         "  tr.prog = prog;\n"
+         "  tr.ordpc = kOrdPc;\n"
+         "  const WoMaterial* m = mats;\n"
+         "#endif\n"
+         "  wodev::pathtrace_block(tr, m, fr, local_rows, out, seg_slots);\n"
+         "}\n",
+         n_recs ? n_recs : 1u, n_mats_used, n_prims ? n_prims : 1u, n_recs * 8u, n_mats_used * 8u, n_prims);
     if (g.err || b.oom) {
         free(b.s);
         return NULL;
