@@ -537,6 +537,7 @@ __global__ __launch_bounds__(kBlock) void assemble_kernel(const float4* __restri
 // ===========================================================================
 struct WoDev {
     int device;
+    int cus;           // compute units (multiProcessorCount)
     std::string arch;  // gcnArchName, e.g. gfx950:sramecc+:xnack-
     WoRec* d_prog;
     size_t prog_cap;
@@ -596,6 +597,7 @@ extern "C" int wo_dev_create(int device, WoDev** out, char* err, size_t errlen) 
         return -1;
     }
     dev->device = device;
+    dev->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 1;
     dev->arch = prop.gcnArchName;
     e = hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -874,6 +876,28 @@ extern "C" void wo_dev_set_lanes(WoDev* dev, int on) {
 }
 extern "C" double wo_dev_jit_compile_sec(WoDev* dev) { return dev ? dev->jit_compile_sec : 0.0; }
 
+// Path-tracer workgroup tile: the largest of 8x8, 8x4 and 4x4 pixels whose grid
+// still fills the device at least 4 times over (`resident` = workgroups the
+// device holds at once), else 4x4.  Bigger tiles keep more lanes busy (more
+// jobs per lane); small ones keep the last workgroups short, which a rank's
+// small share of the frame needs.  Measured on csg32 1920x1080x64: one GPU
+// 8x8 5.54 ms, 8x4 5.68, 4x4 6.11; one rank of 8 (136 rows) 8x8 1.08 ms, 8x4
+// 0.840, 4x4 0.841.  WOLOLO_TILE=8x8|8x4|4x4 forces one.
+static uint32_t pick_tile(uint32_t width, uint32_t rows, uint32_t resident) {
+    static const uint32_t shapes[3][2] = {{3u, 3u}, {3u, 2u}, {2u, 2u}};
+    const char* f = getenv("WOLOLO_TILE");
+    if (f && *f) {
+        if (!strcmp(f, "8x8")) return 3u | (3u << 4);
+        if (!strcmp(f, "8x4")) return 3u | (2u << 4);
+        if (!strcmp(f, "4x4")) return 2u | (2u << 4);
+    }
+    for (const auto& sh : shapes) {
+        uint64_t n = (uint64_t)((width + (1u << sh[0]) - 1u) >> sh[0]) * ((rows + (1u << sh[1]) - 1u) >> sh[1]);
+        if (n >= 4ull * resident) return sh[0] | (sh[1] << 4);
+    }
+    return 2u | (2u << 4);
+}
+
 static const size_t kLdsBudget = 64u * 1024u;
 // Lane-traversal nodes in LDS: up to ~1200 nodes keeps 6 workgroups per CU
 // (24 KB + 7 KB of sample accumulators each).
@@ -908,11 +932,6 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
             snprintf(err, errlen, "scene has %u primitives (max %u)", fr.n_prims, (1u << 20) - 1u);
             return -1;
         }
-        dim3 grid((fr.width + kTileW - 1) / kTileW, (local_rows + kTileH - 1) / kTileH);
-        if (grid.y > 65535u) {
-            snprintf(err, errlen, "frame too tall (%u local rows)", local_rows);
-            return -1;
-        }
         // the kernels count segments into the per-device slots; seg_collect_kernel
         // then moves the sum into the caller's counter
         unsigned long long* slots = nullptr;
@@ -929,28 +948,17 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
             }
             slots = dev->d_segslots;
         }
+        // which kernel, with how much dynamic LDS; then the workgroups one CU holds
+        enum { kLanesLds, kLanesGlobal, kJit, kInterpLds, kInterpGlobal } kind;
+        size_t dyn_lds = 0;
+        KLayout lay = {};
         if (dev->lanes_on && dev->union_only && !dev->jit_fn) {
-            size_t lds = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
-            if (lds <= kLanesLdsBudget)
-                hipLaunchKernelGGL(pathtrace_lanes_kernel<true>, grid, dim3(kBlock), lds, stream, dev->d_prog,
-                                   dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out,
-                                   slots);
-            else
-                hipLaunchKernelGGL(pathtrace_lanes_kernel<false>, grid, dim3(kBlock), 0, stream, dev->d_prog,
-                                   dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out,
-                                   slots);
+            dyn_lds = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
+            kind = dyn_lds <= kLanesLdsBudget ? kLanesLds : kLanesGlobal;
+            if (kind == kLanesGlobal) dyn_lds = 0;
         } else if (dev->jit_fn) {
-            const WoRec* p = dev->d_prog;
-            const WoMaterial* m = dev->d_mats;
-            unsigned long long* s = slots;
-            void* args[] = {&p, &m, &fr, &local_rows, &out, &s};
-            e = hipModuleLaunchKernel(dev->jit_fn, grid.x, grid.y, 1, kBlock, 1, 1, 0, stream, args, nullptr);
-            if (e != hipSuccess) {
-                set_err(err, errlen, "hipModuleLaunchKernel", e);
-                return -1;
-            }
+            kind = kJit;
         } else {
-            KLayout lay;
             lay.codes_words = (fr.n_recs + 7u) / 8u + 1u;
             lay.ordpc_off = lay.codes_words;
             uint32_t hib_words = fr.n_prims > 64u ? (fr.n_prims - 64u + 31u) / 32u : 0u;
@@ -959,15 +967,69 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
             size_t scratch = (size_t)(kBlock / 64u) * lay.wave_words * 4u;
             size_t prog_bytes = (size_t)fr.n_recs * sizeof(WoRec);
             if (prog_bytes + scratch <= kLdsBudget) {
-                hipLaunchKernelGGL(pathtrace_kernel<true>, grid, dim3(kBlock), prog_bytes + scratch, stream,
-                                   dev->d_prog, dev->d_mats, fr, lay, local_rows, out, slots);
+                kind = kInterpLds;
+                dyn_lds = prog_bytes + scratch;
             } else if (scratch <= kLdsBudget) {
-                hipLaunchKernelGGL(pathtrace_kernel<false>, grid, dim3(kBlock), scratch, stream, dev->d_prog,
-                                   dev->d_mats, fr, lay, local_rows, out, slots);
+                kind = kInterpGlobal;
+                dyn_lds = scratch;
             } else {
                 snprintf(err, errlen, "scene too large for the LDS scratch (%zu bytes per workgroup)", scratch);
                 return -1;
             }
+        }
+        int per_cu = 0;
+        switch (kind) {
+        case kLanesLds:
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pathtrace_lanes_kernel<true>, kBlock, dyn_lds);
+            break;
+        case kLanesGlobal:
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pathtrace_lanes_kernel<false>, kBlock, 0);
+            break;
+        case kJit: e = hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dev->jit_fn, kBlock, 0); break;
+        case kInterpLds:
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pathtrace_kernel<true>, kBlock, dyn_lds);
+            break;
+        default:
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pathtrace_kernel<false>, kBlock, dyn_lds);
+            break;
+        }
+        if (e != hipSuccess || per_cu < 1) per_cu = 1;
+        fr.tile_log2 = pick_tile(fr.width, local_rows, (uint32_t)dev->cus * (uint32_t)per_cu);
+        const uint32_t twl = fr.tile_log2 & 15u, thl = fr.tile_log2 >> 4;
+        dim3 grid((fr.width + (1u << twl) - 1u) >> twl, (local_rows + (1u << thl) - 1u) >> thl);
+        if (grid.y > 65535u) {
+            snprintf(err, errlen, "frame too tall (%u local rows)", local_rows);
+            return -1;
+        }
+        switch (kind) {
+        case kLanesLds:
+            hipLaunchKernelGGL(pathtrace_lanes_kernel<true>, grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                               dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots);
+            break;
+        case kLanesGlobal:
+            hipLaunchKernelGGL(pathtrace_lanes_kernel<false>, grid, dim3(kBlock), 0, stream, dev->d_prog, dev->d_trav,
+                               dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots);
+            break;
+        case kJit: {
+            const WoRec* p = dev->d_prog;
+            const WoMaterial* m = dev->d_mats;
+            unsigned long long* sl = slots;
+            void* args[] = {&p, &m, &fr, &local_rows, &out, &sl};
+            e = hipModuleLaunchKernel(dev->jit_fn, grid.x, grid.y, 1, kBlock, 1, 1, 0, stream, args, nullptr);
+            if (e != hipSuccess) {
+                set_err(err, errlen, "hipModuleLaunchKernel", e);
+                return -1;
+            }
+            break;
+        }
+        case kInterpLds:
+            hipLaunchKernelGGL(pathtrace_kernel<true>, grid, dim3(kBlock), dyn_lds, stream, dev->d_prog, dev->d_mats,
+                               fr, lay, local_rows, out, slots);
+            break;
+        default:
+            hipLaunchKernelGGL(pathtrace_kernel<false>, grid, dim3(kBlock), dyn_lds, stream, dev->d_prog, dev->d_mats,
+                               fr, lay, local_rows, out, slots);
+            break;
         }
         if (slots) hipLaunchKernelGGL(seg_collect_kernel, dim3(1), dim3(kBlock), 0, stream, slots, d_segments);
     } else {
