@@ -200,6 +200,9 @@ def main():
                     "kernel_ms": round(k_ms, 4),
                     "flop_per_segment": info.flop_per_segment,
                     "segments_per_launch": segs_local // steps, "trace_path": r.trace_path()}
+            if r.trace_path() == "lanes" or info.spheres + info.halfspaces > 64:
+                roof["note"] = ("flop_per_segment counts every primitive (SURVEY.md 8(d)); BOUND culling skips "
+                                "most of them here, so achieved/frac overstate the VALU work actually done")
         else:
             value = W * H * steps / elapsed_s / 1e6
             bytes_launch = lr * W * 16
