@@ -348,3 +348,18 @@ def test_jit_event_windows(window, monkeypatch):
         ref, _ = _oracle_rows(r, p)
         _cmp(img, ref, f"{name} window={window}")
         r.close()
+
+
+@pytest.mark.parametrize("tile", ["8x8", "8x4", "4x4"])
+@pytest.mark.parametrize("path", PATHS)
+def test_workgroup_tile_shapes(tile, path, monkeypatch):
+    """Every workgroup tile shape the launch can pick gives the oracle's frame, on
+    a frame whose edges cut tiles (odd width, odd height)."""
+    monkeypatch.setenv("WOLOLO_TILE", tile)
+    r, info = _scene("csg32", path)
+    p = info.params(width=77, height=43, spp=3, seed=5)
+    img = r.render(p)
+    _check_path(r, path, "csg32")
+    ref, _ = _oracle_rows(r, p)
+    _cmp(img, ref, f"tile {tile} path={path}")
+    r.close()
