@@ -392,7 +392,7 @@ template <bool kLds>
 __global__ __launch_bounds__(kBlock, WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
     const WoRec* __restrict__ prog, const float4* __restrict__ gnodes, const uint32_t* __restrict__ ordpc,
     const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t ntrav, uint32_t local_rows, float4* __restrict__ out,
-    unsigned long long* __restrict__ seg_slots) {
+    unsigned long long* __restrict__ seg_slots, TileGrid tg) {
     LaneTracer<kLds> tr;
     tr.prog = prog;
     tr.ordpc = ordpc;
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(kBlock, WO_LANES_MIN_WAVES) void pathtrace_lanes_ke
         tr.geo = gnodes;
         tr.aux = gaux;
     }
-    pathtrace_block(tr, mats, fr, local_rows, out, seg_slots);
+    pathtrace_block(tr, mats, fr, local_rows, out, seg_slots, tg);
 }
 
 // ---------------------------------------------------------------------------
@@ -472,7 +472,8 @@ __global__ __launch_bounds__(kBlock) void pathtrace_kernel(const WoRec* __restri
                                                            const WoMaterial* __restrict__ mats, WoFrame fr,
                                                            KLayout lay, uint32_t local_rows,
                                                            float4* __restrict__ out,
-                                                           unsigned long long* __restrict__ seg_slots) {
+                                                           unsigned long long* __restrict__ seg_slots,
+                                                           TileGrid tg) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t nrec = fr.n_recs;
@@ -495,7 +496,7 @@ __global__ __launch_bounds__(kBlock) void pathtrace_kernel(const WoRec* __restri
     tr.ordpc = ws + lay.ordpc_off;
     tr.hib = ws + lay.hib_off;
     tr.lane = lane;
-    pathtrace_block(tr, mats, fr, local_rows, out, seg_slots);
+    pathtrace_block(tr, mats, fr, local_rows, out, seg_slots, tg);
 }
 
 // Sums (and clears) the segment slots into the caller's counter.
@@ -876,26 +877,52 @@ extern "C" void wo_dev_set_lanes(WoDev* dev, int on) {
 }
 extern "C" double wo_dev_jit_compile_sec(WoDev* dev) { return dev ? dev->jit_compile_sec : 0.0; }
 
-// Path-tracer workgroup tile: the largest of 8x8, 8x4 and 4x4 pixels whose grid
-// still fills the device at least 4 times over (`resident` = workgroups the
-// device holds at once), else 4x4.  Bigger tiles keep more lanes busy (more
-// jobs per lane); small ones keep the last workgroups short, which a rank's
-// small share of the frame needs.  Measured on csg32 1920x1080x64: one GPU
-// 8x8 5.54 ms, 8x4 5.68, 4x4 6.11; one rank of 8 (136 rows) 8x8 1.08 ms, 8x4
-// 0.840, 4x4 0.841.  WOLOLO_TILE=8x8|8x4|4x4 forces one.
-static uint32_t pick_tile(uint32_t width, uint32_t rows, uint32_t resident) {
-    static const uint32_t shapes[3][2] = {{3u, 3u}, {3u, 2u}, {2u, 2u}};
+// Path-tracer launch grid (TileGrid): big tiles first, then a tail of small
+// 4x4 tiles sized to ~3 waves of resident workgroups, which fills the end of
+// the frame while the last big tiles finish.  Measured (csg32 1080p64, slowest
+// rank, tools/rank_share.py): no tail 5.57 / 2.87 / 1.60 / 1.09 ms at N = 1 / 2 /
+// 4 / 8 (8x8 tiles throughout); 3-round tail 5.50 / 2.81 / 1.53 / 0.81 ms.  The big shape is 8x8
+// unless the frame is too small for that to fill the device once; `resident` =
+// workgroups the device holds at once.  Env (measurements): WOLOLO_TILE=8x8|8x4|4x4
+// forces one shape everywhere; WOLOLO_TILE_TAIL=<rounds> sets the tail (0: none).
+static uint32_t shape_of(const char* f) {
+    if (!strcmp(f, "8x8")) return 3u | (3u << 4);
+    if (!strcmp(f, "8x4")) return 3u | (2u << 4);
+    if (!strcmp(f, "4x4")) return 2u | (2u << 4);
+    return 0u;
+}
+static uint32_t tiles_across(uint32_t width, uint32_t shape) { return (width + (1u << (shape & 15u)) - 1u) >> (shape & 15u); }
+
+static TileGrid plan_tiles(uint32_t width, uint32_t rows, uint32_t resident) {
+    const uint32_t s44 = 2u | (2u << 4);
+    TileGrid g;
+    g.small_log2 = s44;
+    g.tiles_x_small = tiles_across(width, s44);
+    double tail_rounds = 3.0;
+    const char* tv = getenv("WOLOLO_TILE_TAIL");
+    if (tv && *tv) tail_rounds = atof(tv);
     const char* f = getenv("WOLOLO_TILE");
-    if (f && *f) {
-        if (!strcmp(f, "8x8")) return 3u | (3u << 4);
-        if (!strcmp(f, "8x4")) return 3u | (2u << 4);
-        if (!strcmp(f, "4x4")) return 2u | (2u << 4);
+    uint32_t big = (f && *f) ? shape_of(f) : 0u;
+    if (big) {
+        tail_rounds = 0.0;
+    } else {
+        big = 3u | (3u << 4);
+        if ((uint64_t)tiles_across(width, big) * (rows >> 3) < resident) big = 3u | (2u << 4);
+        if ((uint64_t)tiles_across(width, big) * (rows >> 2) < resident) big = s44;
     }
-    for (const auto& sh : shapes) {
-        uint64_t n = (uint64_t)((width + (1u << sh[0]) - 1u) >> sh[0]) * ((rows + (1u << sh[1]) - 1u) >> sh[1]);
-        if (n >= 4ull * resident) return sh[0] | (sh[1] << 4);
+    g.big_log2 = big;
+    g.tiles_x_big = tiles_across(width, big);
+    const uint32_t bh = 1u << (big >> 4);
+    uint32_t rows_small = 0;
+    if (tail_rounds > 0.0 && big != s44) {
+        uint64_t want = (uint64_t)(tail_rounds * resident + 0.5);
+        rows_small = (uint32_t)(((want + g.tiles_x_small - 1u) / g.tiles_x_small) * 4u);
     }
-    return 2u | (2u << 4);
+    uint32_t rows_big = rows > rows_small ? ((rows - rows_small) / bh) * bh : 0u;
+    if (big == s44) rows_big = ((rows + 3u) / 4u) * 4u;  // one shape: the big grid covers everything
+    g.rows_big = rows_big;
+    g.n_big = g.tiles_x_big * (rows_big / bh);
+    return g;
 }
 
 static const size_t kLdsBudget = 64u * 1024u;
@@ -994,28 +1021,31 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
             break;
         }
         if (e != hipSuccess || per_cu < 1) per_cu = 1;
-        fr.tile_log2 = pick_tile(fr.width, local_rows, (uint32_t)dev->cus * (uint32_t)per_cu);
-        const uint32_t twl = fr.tile_log2 & 15u, thl = fr.tile_log2 >> 4;
-        dim3 grid((fr.width + (1u << twl) - 1u) >> twl, (local_rows + (1u << thl) - 1u) >> thl);
-        if (grid.y > 65535u) {
-            snprintf(err, errlen, "frame too tall (%u local rows)", local_rows);
+        const TileGrid tg = plan_tiles(fr.width, local_rows, (uint32_t)dev->cus * (uint32_t)per_cu);
+        const uint64_t n_small =
+            local_rows > tg.rows_big ? (uint64_t)tg.tiles_x_small * ((local_rows - tg.rows_big + 3u) / 4u) : 0u;
+        const uint64_t n_wg = (uint64_t)tg.n_big + n_small;
+        if (n_wg >= (1ull << 31)) {
+            snprintf(err, errlen, "frame too large (%llu workgroups)", (unsigned long long)n_wg);
             return -1;
         }
+        dim3 grid((uint32_t)n_wg);
         switch (kind) {
         case kLanesLds:
             hipLaunchKernelGGL(pathtrace_lanes_kernel<true>, grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                               dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots);
+                               dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg);
             break;
         case kLanesGlobal:
             hipLaunchKernelGGL(pathtrace_lanes_kernel<false>, grid, dim3(kBlock), 0, stream, dev->d_prog, dev->d_trav,
-                               dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots);
+                               dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg);
             break;
         case kJit: {
             const WoRec* p = dev->d_prog;
             const WoMaterial* m = dev->d_mats;
             unsigned long long* sl = slots;
-            void* args[] = {&p, &m, &fr, &local_rows, &out, &sl};
-            e = hipModuleLaunchKernel(dev->jit_fn, grid.x, grid.y, 1, kBlock, 1, 1, 0, stream, args, nullptr);
+            TileGrid tgv = tg;
+            void* args[] = {&p, &m, &fr, &local_rows, &out, &sl, &tgv};
+            e = hipModuleLaunchKernel(dev->jit_fn, grid.x, 1, 1, kBlock, 1, 1, 0, stream, args, nullptr);
             if (e != hipSuccess) {
                 set_err(err, errlen, "hipModuleLaunchKernel", e);
                 return -1;
@@ -1024,11 +1054,11 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
         }
         case kInterpLds:
             hipLaunchKernelGGL(pathtrace_kernel<true>, grid, dim3(kBlock), dyn_lds, stream, dev->d_prog, dev->d_mats,
-                               fr, lay, local_rows, out, slots);
+                               fr, lay, local_rows, out, slots, tg);
             break;
         default:
             hipLaunchKernelGGL(pathtrace_kernel<false>, grid, dim3(kBlock), dyn_lds, stream, dev->d_prog, dev->d_mats,
-                               fr, lay, local_rows, out, slots);
+                               fr, lay, local_rows, out, slots, tg);
             break;
         }
         if (slots) hipLaunchKernelGGL(seg_collect_kernel, dim3(1), dim3(kBlock), 0, stream, slots, d_segments);

@@ -110,9 +110,7 @@ typedef struct WoFrame {
     uint32_t n_prims;           /* primitive count */
     float time_sec;             /* ubershader: UBO time_since_start_sec */
     float sphere_y;             /* ubershader: 2*sin(omega*time), hoisted to the host */
-    uint32_t tile_log2;         /* path tracer workgroup tile: log2 width | log2 height << 4
-                                 * (set at launch; the image does not depend on it) */
-    float pad;
+    float pad[2];
     WoCamera cam;
 } WoFrame;
 
