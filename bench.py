@@ -37,7 +37,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scene", default="csg32",
-                    choices=["csg32", "rtiow_cover", "csg256_balanced", "csg256_chain", "csg32_union", "sphere256"])
+                    choices=["csg32", "rtiow_cover", "csg256_balanced", "csg256_chain", "csg32_union", "csg256_balanced_union",
+                             "sphere256"])
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)

@@ -301,12 +301,14 @@ struct LaneTracer {
                 const uint32_t a = aux[pc];
                 const float4 g = geo[pc];
                 const uint32_t kind = a >> 30, val = a & 0x3fffffffu;
+                // BOUND and sphere nodes share the centre-to-line arithmetic, so lanes
+                // at different node kinds run it once: b = (o - c).d, ll = distance^2
+                // (a generic primitive's lanes compute it and ignore it)
+                float b, ll;
+                sphere_bl(g.x, g.y, g.z, o, d, b, ll);
                 if (kind == kNodeBound) {
-                    float ox = g.x - o.x, oy = g.y - o.y, oz = g.z - o.z;
-                    float tca = __builtin_fmaf(oz, d.z, __builtin_fmaf(oy, d.y, ox * d.x));
-                    float lx = __builtin_fmaf(-tca, d.x, ox), ly = __builtin_fmaf(-tca, d.y, oy),
-                          lz = __builtin_fmaf(-tca, d.z, oz);
-                    float d2 = __builtin_fmaf(lz, lz, __builtin_fmaf(ly, ly, lx * lx));
+                    // tca = (c - o).d = -b; ll is the same bits either way
+                    const float tca = -b, d2 = ll;
                     bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, g.w * g.w)) || (tca + g.w < 0.0f);
                     // near end of the sphere along the ray, rounded down generously
                     float lo = (tca - g.w) - 1e-5f * (fabsf(tca) + g.w);
@@ -321,7 +323,7 @@ struct LaneTracer {
                     Ivl iv;
                     if (kind == kNodeSphere) {
                         float la, lb;
-                        sphere_interval(g.x, g.y, g.z, g.w, o, d, la, lb);
+                        sphere_interval_bl(b, ll, g.w, la, lb);
                         ivl_first(iv, la, lb);
                     } else {
                         const uint32_t ppc = ordpc[val];

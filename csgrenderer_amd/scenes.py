@@ -234,7 +234,7 @@ def build_csg32(r: Renderer, seed: int = 32, width=1920, height=1080, spp=64, un
 
 
 def build_csg256(r: Renderer, seed: int = 256, shape: str = "balanced", width=1920, height=1080,
-                 spp=64) -> SceneInfo:
+                 spp=64, union_only=False) -> SceneInfo:
     """C5: 128 sphere leaves, 127 binops (255 nodes), leaf 0 an RTIOW-style ground
     sphere (r = 1000).
       balanced: 63 overlapping pairs (ops cycle u/d/i) + ground + 1 sphere, joined
@@ -247,7 +247,7 @@ def build_csg256(r: Renderer, seed: int = 256, shape: str = "balanced", width=19
     gitem = (ground, (0.0, -1000.0, 0.0))
     if shape == "balanced":
         items = [gitem] + _overlapping_pairs(r, rng, 63, (-5.0, 0.3, -5.0), (5.0, 2.5, 5.0), 0.25, 0.6,
-                                               _cycle("udi"))
+                                               _cycle("uui" if union_only else "udi"))
         s = r.sphere(1.0)
         r.set_material(s, r.dielectric(1.5))
         items.append((s, (0.0, 1.0, 0.0)))
@@ -266,7 +266,7 @@ def build_csg256(r: Renderer, seed: int = 256, shape: str = "balanced", width=19
     else:
         raise ValueError(shape)
     r.set_camera((0.0, 6.0, 13.0), (0.0, 0.8, 0.0), (0, 1, 0), 45.0, 0.0, 13.0)
-    return SceneInfo(f"csg256_{shape}", spheres=128, halfspaces=0, binops=127, width=width, height=height, spp=spp,
+    return SceneInfo(f"csg256_{shape}" + ("_union" if union_only else ""), spheres=128, halfspaces=0, binops=127, width=width, height=height, spp=spp,
                      max_depth=8)
 
 
@@ -276,6 +276,7 @@ SCENES = {
     # csg32's geometry with the differences made unions (an A/B scene for the
     # union-only lane tracer; not a BASELINE config)
     "csg32_union": lambda r, **k: build_csg32(r, union_only=True, **k),
+    "csg256_balanced_union": lambda r, **k: build_csg256(r, shape="balanced", union_only=True, **k),
     "csg256_balanced": lambda r, **k: build_csg256(r, shape="balanced", **k),
     "csg256_chain": lambda r, **k: build_csg256(r, shape="chain", **k),
 }

@@ -90,7 +90,7 @@ int wo_renderer_frame_desc(Wo_Renderer* r, Wo_RenderParams const* params, uint32
                            uint32_t rank, uint32_t nranks, WoFrame* out);
 
 /* Path-tracer kernel selection (results are identical; only speed differs).
- *   AUTO         union-only scenes of more than WOLOLO_LANES_MIN_PRIMS (64)
+ *   AUTO         union-only scenes of more than WOLOLO_LANES_MIN_PRIMS (256)
  *                primitives -> LANES; else scenes of up to WOLOLO_JIT_MAX_PRIMS
  *                (256) primitives -> JIT; else INTERPRETER.
  *   INTERPRETER  the postfix-program interpreter kernel.

@@ -310,7 +310,9 @@ def _union_scene(n_spheres=90):
 
 
 @pytest.mark.parametrize("tracer", ["lanes", "auto"])
-def test_lanes_union_scene_bitexact(tracer):
+def test_lanes_union_scene_bitexact(tracer, monkeypatch):
+    # AUTO takes the lane tracer for union-only scenes above WOLOLO_LANES_MIN_PRIMS (256 by default)
+    monkeypatch.setenv("WOLOLO_LANES_MIN_PRIMS", "64")
     r = _union_scene()
     assert _union_only(r) and r.program()[2] > 64
     r.set_tracer(tracer)
@@ -324,8 +326,9 @@ def test_lanes_union_scene_bitexact(tracer):
 
 
 def test_auto_tracer_choices():
-    """AUTO: the RTIOW cover (union-only, 487 primitives) takes the lane tracer; csg32 the JIT."""
-    for name, want in [("rtiow_cover", "lanes"), ("csg32", "jit")]:
+    """AUTO: the RTIOW cover (union-only, 487 primitives) takes the lane tracer; csg32 and a
+    128-primitive union-only scene the JIT."""
+    for name, want in [("rtiow_cover", "lanes"), ("csg32", "jit"), ("csg256_balanced_union", "jit")]:
         r, info = _scene(name, "auto")
         r.render(info.params(width=32, height=18, spp=1))
         assert r.trace_path() == want, (name, r.trace_path())
