@@ -262,6 +262,9 @@ Wo_Material wo_renderer_add_dielectric_material(Wo_Renderer* r, Wo_Scalar refrac
     m.kind = WO_MAT_DIELECTRIC;
     m.albedo[0] = m.albedo[1] = m.albedo[2] = 1.0f;
     m.ior = (float)refraction_index;
+    m.inv_ior = (float)(1.0 / refraction_index);
+    const double q = (1.0 - refraction_index) / (1.0 + refraction_index);
+    m.r0 = (float)(q * q);
     return add_material(r, &m);
 }
 
@@ -339,6 +342,8 @@ int wo_renderer_frame_desc(Wo_Renderer* r, Wo_RenderParams const* p, uint32_t ti
     out->n_prims = r->n_prims;
     out->time_sec = p->time_sec;
     out->sphere_y = ubershader_sphere_y(p->time_sec);
+    out->inv_width = p->width ? 1.0f / (float)p->width : 0.0f;
+    out->inv_height = p->height ? 1.0f / (float)p->height : 0.0f;
     wo_resolve_camera(&r->camera, p->width, p->height, &out->cam);
     return 0;
 }

@@ -74,7 +74,8 @@ typedef struct WoMaterial {
     float albedo[3];
     float fuzz;   /* metal */
     float ior;    /* dielectric refraction index */
-    float pad[2];
+    float inv_ior; /* dielectric: 1/ior, rounded from double on the host */
+    float r0;      /* dielectric: Schlick's ((1-ior)/(1+ior))^2, rounded from double on the host */
 } WoMaterial;
 
 /* Shading modes (Wo_ShadingMode in renderer_ext.h uses the same values). */
@@ -110,7 +111,7 @@ typedef struct WoFrame {
     uint32_t n_prims;           /* primitive count */
     float time_sec;             /* ubershader: UBO time_since_start_sec */
     float sphere_y;             /* ubershader: 2*sin(omega*time), hoisted to the host */
-    float pad[2];
+    float inv_width, inv_height; /* path tracer: 1/width, 1/height (fp32); sample position = (x + jitter) * inv_width */
     WoCamera cam;
 } WoFrame;
 

@@ -456,13 +456,13 @@ static void shade_pixel(const WoRec* prog, uint32_t n, const WoMaterial* mats, u
         uint32_t rng = oracle_pcg_hash(pixel ^ oracle_pcg_hash((fr->sample_offset + smp) ^ oracle_pcg_hash(fr->seed)));
         float u, v;
         if (normals) {
-            u = ((float)x + 0.5f) / (float)W;
-            v = ((float)(H - 1u - y) + 0.5f) / (float)H;
+            u = ((float)x + 0.5f) * fr->inv_width;
+            v = ((float)(H - 1u - y) + 0.5f) * fr->inv_height;
         } else {
             float jx = rng_float(&rng);
             float jy = rng_float(&rng);
-            u = ((float)x + jx) / (float)W;
-            v = ((float)(H - 1u - y) + jy) / (float)H;
+            u = ((float)x + jx) * fr->inv_width;
+            v = ((float)(H - 1u - y) + jy) * fr->inv_height;
         }
         float off[3] = {0.0f, 0.0f, 0.0f};
         if (cam->lens_radius > 0.0f && !normals) {
@@ -538,15 +538,14 @@ static void shade_pixel(const WoRec* prog, uint32_t n, const WoMaterial* mats, u
                 normalize3(nd);
                 for (int i = 0; i < 3; ++i) att[i] = m->albedo[i];
             } else {
-                float ri = front ? (1.0f / m->ior) : m->ior;
+                float ri = front ? m->inv_ior : m->ior;
                 float nd0[3] = {-d[0], -d[1], -d[2]};
                 float ct = dot3(nd0, N);
                 if (!(ct < 1.0f)) ct = 1.0f;
                 float st = sqrtf(1.0f - ct * ct);
                 int reflect = ri * st > 1.0f;
                 if (!reflect) {
-                    float r0 = (1.0f - ri) / (1.0f + ri);
-                    r0 = r0 * r0;
+                    const float r0 = m->r0; /* Schlick base, symmetric in ri and 1/ri */
                     float q = 1.0f - ct;
                     float q5 = (((q * q) * q) * q) * q;
                     reflect = r0 + (1.0f - r0) * q5 > rng_float(&rng);
