@@ -100,6 +100,7 @@ Wo_Renderer* wo_renderer_new(Wo_App* app, char const* name, size_t max_node_coun
     }
     r->t0 = wo_monotonic_sec();
     r->dirty = 1;
+    r->view_version++;
     {
         const char* j = getenv("WOLOLO_JIT");
         const char* t = getenv("WOLOLO_TRACER");
@@ -137,12 +138,12 @@ Wo_Renderer* wo_renderer_new(Wo_App* app, char const* name, size_t max_node_coun
 
 void wo_renderer_del(Wo_Renderer* r) {
     if (!r) return;
+    (void)wo_renderer_finish(r);
     if (r->dev) wo_dev_destroy(r->dev);
     free(r->nodes);
     free(r->nonroot);
     free(r->mats);
     free(r->prog);
-    free(r->host_frame);
     free(r->name);
     free(r);
 }
@@ -161,6 +162,7 @@ static Wo_Node alloc_node(Wo_Renderer* r, uint32_t kind) {
     r->nodes[n].kind = kind;
     r->nodes[n].material = 0;
     r->dirty = 1;
+    r->view_version++;
     return n;
 }
 
@@ -232,6 +234,7 @@ static Wo_Material add_material(Wo_Renderer* r, WoMaterial const* m) {
     }
     r->mats[r->n_mats] = *m;
     r->dirty = 1;
+    r->view_version++;
     return r->n_mats++;
 }
 
@@ -274,6 +277,7 @@ bool wo_renderer_set_node_material(Wo_Renderer* r, Wo_Node leaf, Wo_Material mat
     if (k != WO_NODE_SPHERE && k != WO_NODE_HALFSPACE) return false;
     r->nodes[leaf].material = material;
     r->dirty = 1;
+    r->view_version++;
     return true;
 }
 
@@ -285,6 +289,7 @@ void wo_renderer_set_camera(Wo_Renderer* r, Wo_Vec3 look_from, Wo_Vec3 look_at, 
     r->camera.vfov_deg = vertical_fov_deg;
     r->camera.aperture = aperture;
     r->camera.focus_dist = focus_dist;
+    r->view_version++;
 }
 
 void wo_renderer_set_draw_params(Wo_Renderer* r, Wo_RenderParams const* params, int pin_time) {
@@ -484,25 +489,133 @@ static void write_ppm(const char* path, const float* rgba, uint32_t w, uint32_t 
     fclose(f);
 }
 
+/* Present a finished frame: keep it as the last frame and dump it when
+ * WOLOLO_OUTPUT names a file (the headless stand-in for the swapchain). */
+static void present(Wo_Renderer* r, float const* px, uint32_t w, uint32_t h) {
+    r->last_frame = px;
+    r->last_w = w;
+    r->last_h = h;
+    r->frames_drawn++;
+    const char* out = getenv("WOLOLO_OUTPUT");
+    if (out && *out) write_ppm(out, px, w, h);
+}
+
+static int retire_slot(Wo_Renderer* r, int slot) {
+    if (!r->pending[slot]) return 0;
+    char err[256] = {0};
+    float const* px = NULL;
+    r->pending[slot] = 0;
+    if (wo_dev_frame_wait(r->dev, slot, &px, err, sizeof err)) {
+        wo_set_error("frame wait failed: %s", err);
+        return -1;
+    }
+    present(r, px, r->pend_w[slot], r->pend_h[slot]);
+    return 0;
+}
+
+int wo_renderer_finish(Wo_Renderer* r) {
+    if (!r || !r->dev) return 0;
+    /* oldest first: the slot not used by the newest submission */
+    int newest = (int)((r->frame_seq + 1u) & 1u);
+    int rc = retire_slot(r, newest ^ 1);
+    if (retire_slot(r, newest)) rc = -1;
+    return rc;
+}
+
+/* Accumulation bookkeeping shared by draw_frame and render_accumulate: whether
+ * this frame continues the accumulation, its sample offset and the total. */
+static int acc_continues(Wo_Renderer* r, Wo_RenderParams const* p) {
+    Wo_RenderParams a = r->acc_params;
+    return r->acc_valid && r->acc_view == r->view_version && a.width == p->width && a.height == p->height &&
+           a.spp == p->spp && a.max_depth == p->max_depth && a.seed == p->seed && a.mode == p->mode &&
+           a.sample_offset == p->sample_offset;
+}
+
+static int submit_frame(Wo_Renderer* r, Wo_RenderParams p, int slot, int accumulate, int reset) {
+    char err[256] = {0};
+    long long* d_acc = NULL;
+    uint32_t total = 0;
+    if (accumulate && p.mode == WO_SHADING_PATHTRACE) {
+        int cont = !reset && acc_continues(r, &p);
+        if (!cont) {
+            r->acc_params = p;
+            r->acc_view = r->view_version;
+            r->acc_spp = 0;
+            r->acc_valid = 1;
+        }
+        if (wo_dev_accum_prepare(r->dev, p.width, p.height, !cont, &d_acc, err, sizeof err)) {
+            wo_set_error("accumulation buffer: %s", err);
+            return -1;
+        }
+        uint64_t t = (uint64_t)r->acc_spp + p.spp;
+        if (t > 0xFFFFFFFFull) {
+            wo_set_error("accumulated samples overflow");
+            return -1;
+        }
+        p.sample_offset = r->acc_params.sample_offset + r->acc_spp;
+        total = (uint32_t)t;
+        r->acc_spp = total;
+    }
+    WoFrame fr;
+    if (wo_renderer_frame_desc(r, &p, 4, 0, 1, &fr)) return -1;
+    if (wo_dev_frame_submit(r->dev, &fr, slot, d_acc, total, err, sizeof err)) {
+        wo_set_error("frame submit failed: %s", err);
+        return -1;
+    }
+    r->pending[slot] = 1;
+    r->pend_w[slot] = p.width;
+    r->pend_h[slot] = p.height;
+    return 0;
+}
+
+/* Reference draw_frame_with_renderer (renderer.c:2085-2219) waits for the queue
+ * every frame (vkQueueWaitIdle, 2212).  Here frame k is submitted (render + copy
+ * to pinned host memory, asynchronous) and then frame k-1 is waited for and
+ * presented, so the GPU renders frame k while the host presents k-1. */
 void wo_renderer_draw_frame(Wo_Renderer* r) {
     if (!r) return;
     Wo_RenderParams p = r->draw;
     if (!r->pin_time) p.time_sec = (float)(r->app ? wo_app_time_sec(r->app) : wo_monotonic_sec() - r->t0);
-    size_t need = (size_t)p.width * p.height * 4;
-    if (need > r->host_frame_cap) {
-        free(r->host_frame);
-        r->host_frame = (float*)malloc(need * sizeof(float));
-        r->host_frame_cap = r->host_frame ? need : 0;
-        if (!r->host_frame) {
-            fprintf(stderr, WO_LOG_PREFIX " out of host memory for the framebuffer\n");
-            return;
-        }
-    }
-    if (wo_renderer_render_f32(r, &p, r->host_frame) != 0) {
+    if (sync_device(r)) {
         fprintf(stderr, WO_LOG_PREFIX " draw_frame failed: %s\n", wo_renderer_last_error());
         return;
     }
-    r->frames_drawn++;
-    const char* out = getenv("WOLOLO_OUTPUT");
-    if (out && *out) write_ppm(out, r->host_frame, p.width, p.height);
+    int slot = (int)(r->frame_seq & 1u);
+    if (retire_slot(r, slot) == 0 && submit_frame(r, p, slot, r->progressive, 0) == 0) {
+        r->frame_seq++;
+        if (retire_slot(r, slot ^ 1) == 0) return;
+    }
+    fprintf(stderr, WO_LOG_PREFIX " draw_frame failed: %s\n", wo_renderer_last_error());
+}
+
+void wo_renderer_set_progressive(Wo_Renderer* r, int on) {
+    r->progressive = on != 0;
+    if (!on) r->acc_valid = 0;
+}
+
+uint32_t wo_renderer_accumulated_spp(Wo_Renderer* r) { return r->acc_valid ? r->acc_spp : 0u; }
+
+float const* wo_renderer_last_frame(Wo_Renderer* r, uint32_t* width, uint32_t* height) {
+    if (width) *width = r->last_frame ? r->last_w : 0u;
+    if (height) *height = r->last_frame ? r->last_h : 0u;
+    return r->last_frame;
+}
+
+int wo_renderer_render_accumulate(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba, int reset) {
+    if (params->mode != WO_SHADING_PATHTRACE) {
+        wo_set_error("render_accumulate needs WO_SHADING_PATHTRACE");
+        return -1;
+    }
+    if (wo_renderer_finish(r)) return -1; /* the pipeline's frames first */
+    if (sync_device(r)) return -1;
+    if (submit_frame(r, *params, 0, 1, reset)) return -1;
+    r->pending[0] = 0;
+    char err[256] = {0};
+    float const* px = NULL;
+    if (wo_dev_frame_wait(r->dev, 0, &px, err, sizeof err)) {
+        wo_set_error("frame wait failed: %s", err);
+        return -1;
+    }
+    if (out_rgba) memcpy(out_rgba, px, (size_t)params->width * params->height * 4u * sizeof(float));
+    return (int)r->acc_spp;
 }

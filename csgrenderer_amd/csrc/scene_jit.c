@@ -385,7 +385,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     bput(&b,
          "extern \"C\" __global__ __launch_bounds__(256, WO_JIT_MIN_WAVES) void wo_jit_pathtrace(\n"
          "    const WoRec* __restrict__ prog, const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t local_rows,\n"
-         "    float4* __restrict__ out, unsigned long long* __restrict__ seg_slots, wodev::TileGrid tg) {\n"
+         "    float4* __restrict__ out, unsigned long long* __restrict__ seg_slots, wodev::PathLaunch tg) {\n"
          "  JitTracer tr;\n"
          "#if WO_JIT_LDS_EVENTS\n"
          "  __shared__ uint64_t s_ev[wodev::kLdsEvents * wodev::kBlock];\n"

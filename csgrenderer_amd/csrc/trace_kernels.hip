@@ -394,7 +394,7 @@ template <bool kLds>
 __global__ __launch_bounds__(kBlock, WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
     const WoRec* __restrict__ prog, const float4* __restrict__ gnodes, const uint32_t* __restrict__ ordpc,
     const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t ntrav, uint32_t local_rows, float4* __restrict__ out,
-    unsigned long long* __restrict__ seg_slots, TileGrid tg) {
+    unsigned long long* __restrict__ seg_slots, PathLaunch tg) {
     LaneTracer<kLds> tr;
     tr.prog = prog;
     tr.ordpc = ordpc;
@@ -475,7 +475,7 @@ __global__ __launch_bounds__(kBlock) void pathtrace_kernel(const WoRec* __restri
                                                            KLayout lay, uint32_t local_rows,
                                                            float4* __restrict__ out,
                                                            unsigned long long* __restrict__ seg_slots,
-                                                           TileGrid tg) {
+                                                           PathLaunch tg) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t nrec = fr.n_recs;
@@ -557,6 +557,15 @@ struct WoDev {
     size_t ordpc_cap;
     uint32_t n_trav;
     unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
+    // progressive accumulation (3 int64 per pixel) and the draw_frame pipeline:
+    // two frame slots, each a device frame, a pinned host copy and an event
+    long long* d_accum;
+    size_t accum_cap;
+    float4* d_slot[2];
+    size_t dslot_cap[2];
+    float* h_slot[2];
+    size_t hslot_cap[2];
+    hipEvent_t slot_ev[2];
     bool union_only;
     bool lanes_on;
     // scene-specialised kernel (hiprtc)
@@ -622,6 +631,12 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
     if (dev->d_trav) (void)hipFree(dev->d_trav);
     if (dev->d_ordpc) (void)hipFree(dev->d_ordpc);
     if (dev->d_segslots) (void)hipFree(dev->d_segslots);
+    if (dev->d_accum) (void)hipFree(dev->d_accum);
+    for (int i = 0; i < 2; ++i) {
+        if (dev->d_slot[i]) (void)hipFree(dev->d_slot[i]);
+        if (dev->h_slot[i]) (void)hipHostFree(dev->h_slot[i]);
+        if (dev->slot_ev[i]) (void)hipEventDestroy(dev->slot_ev[i]);
+    }
     if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
     (void)hipStreamDestroy(dev->stream);
     delete dev;
@@ -879,7 +894,7 @@ extern "C" void wo_dev_set_lanes(WoDev* dev, int on) {
 }
 extern "C" double wo_dev_jit_compile_sec(WoDev* dev) { return dev ? dev->jit_compile_sec : 0.0; }
 
-// Path-tracer launch grid (TileGrid): big tiles first, then a tail of small
+// Path-tracer launch grid (PathLaunch): big tiles first, then a tail of small
 // 4x4 tiles sized to ~3 waves of resident workgroups, which fills the end of
 // the frame while the last big tiles finish.  Measured (csg32 1080p64, slowest
 // rank, tools/rank_share.py): no tail 5.57 / 2.87 / 1.60 / 1.09 ms at N = 1 / 2 /
@@ -895,9 +910,9 @@ static uint32_t shape_of(const char* f) {
 }
 static uint32_t tiles_across(uint32_t width, uint32_t shape) { return (width + (1u << (shape & 15u)) - 1u) >> (shape & 15u); }
 
-static TileGrid plan_tiles(uint32_t width, uint32_t rows, uint32_t resident) {
+static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident) {
     const uint32_t s44 = 2u | (2u << 4);
-    TileGrid g;
+    PathLaunch g = {};
     g.small_log2 = s44;
     g.tiles_x_small = tiles_across(width, s44);
     double tail_rounds = 3.0;
@@ -934,6 +949,12 @@ static const size_t kLanesLdsBudget = 24u * 1024u;
 
 extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, void* stream_v,
                              unsigned long long* d_segments, char* err, size_t errlen) {
+    return wo_dev_launch_ex(dev, frame_in, d_out, stream_v, d_segments, nullptr, 0u, err, errlen);
+}
+
+extern "C" int wo_dev_launch_ex(WoDev* dev, WoFrame const* frame_in, void* d_out, void* stream_v,
+                                unsigned long long* d_segments, long long* d_accum, uint32_t accum_spp, char* err,
+                                size_t errlen) {
     hipStream_t stream = (hipStream_t)stream_v;  // NULL = the null stream (HIP convention)
     WoFrame fr = *frame_in;
     if (fr.width == 0 || fr.height == 0) return 0;
@@ -1023,7 +1044,11 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
             break;
         }
         if (e != hipSuccess || per_cu < 1) per_cu = 1;
-        const TileGrid tg = plan_tiles(fr.width, local_rows, (uint32_t)dev->cus * (uint32_t)per_cu);
+        PathLaunch tg = plan_tiles(fr.width, local_rows, (uint32_t)dev->cus * (uint32_t)per_cu);
+        if (d_accum && fr.mode == WO_MODE_PATHTRACE) {
+            tg.acc = d_accum;
+            tg.acc_spp = accum_spp;
+        }
         const uint64_t n_small =
             local_rows > tg.rows_big ? (uint64_t)tg.tiles_x_small * ((local_rows - tg.rows_big + 3u) / 4u) : 0u;
         const uint64_t n_wg = (uint64_t)tg.n_big + n_small;
@@ -1045,8 +1070,8 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
             const WoRec* p = dev->d_prog;
             const WoMaterial* m = dev->d_mats;
             unsigned long long* sl = slots;
-            TileGrid tgv = tg;
-            void* args[] = {&p, &m, &fr, &local_rows, &out, &sl, &tgv};
+            PathLaunch plv = tg;
+            void* args[] = {&p, &m, &fr, &local_rows, &out, &sl, &plv};
             e = hipModuleLaunchKernel(dev->jit_fn, grid.x, 1, 1, kBlock, 1, 1, 0, stream, args, nullptr);
             if (e != hipSuccess) {
                 set_err(err, errlen, "hipModuleLaunchKernel", e);
@@ -1097,6 +1122,105 @@ extern "C" int wo_dev_render_host(WoDev* dev, WoFrame const* frame, float* host_
         set_err(err, errlen, "render (device->host)", e);
         return -1;
     }
+    return 0;
+}
+
+// ---- progressive accumulation and the draw_frame pipeline (renderer.c) ----
+
+// Frames of the pipeline are whole frames (one rank, 4-row tiles).
+static WoFrame whole_frame(WoFrame const* f) {
+    WoFrame fr = *f;
+    fr.tile_rows = 4;
+    fr.rank = 0;
+    fr.nranks = 1;
+    return fr;
+}
+
+extern "C" int wo_dev_accum_prepare(WoDev* dev, uint32_t width, uint32_t height, int reset, long long** d_accum,
+                                    char* err, size_t errlen) {
+    hipError_t e = hipSetDevice(dev->device);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipSetDevice", e);
+        return -1;
+    }
+    const size_t bytes = (size_t)width * wo_rank_local_rows(height, 4u, 1u) * 3u * sizeof(long long);
+    const long long* old = dev->d_accum;
+    if (ensure_buffer(&dev->d_accum, &dev->accum_cap, bytes, err, errlen)) return -1;
+    if (reset || dev->d_accum != old) {
+        e = hipMemsetAsync(dev->d_accum, 0, bytes, dev->stream);
+        if (e != hipSuccess) {
+            set_err(err, errlen, "hipMemsetAsync(accumulation)", e);
+            return -1;
+        }
+    }
+    *d_accum = dev->d_accum;
+    return 0;
+}
+
+extern "C" int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, long long* d_accum,
+                                   uint32_t accum_spp, char* err, size_t errlen) {
+    if (slot < 0 || slot > 1) {
+        snprintf(err, errlen, "bad frame slot %d", slot);
+        return -1;
+    }
+    WoFrame fr = whole_frame(frame);
+    hipError_t e = hipSetDevice(dev->device);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipSetDevice", e);
+        return -1;
+    }
+    const size_t pixels = (size_t)fr.width * fr.height;
+    const size_t dbytes = (size_t)fr.width * wo_rank_local_rows(fr.height, fr.tile_rows, 1u) * sizeof(float4);
+    if (ensure_buffer(&dev->d_slot[slot], &dev->dslot_cap[slot], dbytes, err, errlen)) return -1;
+    if (pixels * sizeof(float4) > dev->hslot_cap[slot] || !dev->h_slot[slot]) {
+        if (dev->h_slot[slot]) (void)hipHostFree(dev->h_slot[slot]);
+        dev->h_slot[slot] = nullptr;
+        dev->hslot_cap[slot] = 0;
+        e = hipHostMalloc((void**)&dev->h_slot[slot], pixels ? pixels * sizeof(float4) : 64, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            dev->h_slot[slot] = nullptr;
+            set_err(err, errlen, "hipHostMalloc(frame slot)", e);
+            return -1;
+        }
+        dev->hslot_cap[slot] = pixels * sizeof(float4);
+    }
+    if (!dev->slot_ev[slot]) {
+        e = hipEventCreateWithFlags(&dev->slot_ev[slot], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            dev->slot_ev[slot] = nullptr;
+            set_err(err, errlen, "hipEventCreate", e);
+            return -1;
+        }
+    }
+    if (wo_dev_launch_ex(dev, &fr, dev->d_slot[slot], dev->stream, nullptr, d_accum, accum_spp, err, errlen))
+        return -1;
+    if (pixels) {
+        e = hipMemcpyAsync(dev->h_slot[slot], dev->d_slot[slot], pixels * sizeof(float4), hipMemcpyDeviceToHost,
+                           dev->stream);
+        if (e != hipSuccess) {
+            set_err(err, errlen, "hipMemcpyAsync(frame slot)", e);
+            return -1;
+        }
+    }
+    e = hipEventRecord(dev->slot_ev[slot], dev->stream);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipEventRecord", e);
+        return -1;
+    }
+    return 0;
+}
+
+extern "C" int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, char* err, size_t errlen) {
+    if (slot < 0 || slot > 1 || !dev->slot_ev[slot]) {
+        snprintf(err, errlen, "frame slot %d was never submitted", slot);
+        return -1;
+    }
+    hipError_t e = hipEventSynchronize(dev->slot_ev[slot]);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "frame wait", e);
+        return -1;
+    }
+    *host = dev->h_slot[slot];
     return 0;
 }
 

@@ -40,6 +40,25 @@ double wo_dev_jit_compile_sec(WoDev* dev);
 /* Launch the frame's kernel for this rank's tiles into d_out on `stream` (async). */
 int wo_dev_launch(WoDev* dev, WoFrame const* frame, void* d_out, void* stream,
                   unsigned long long* d_segments, char* err, size_t errlen);
+/* wo_dev_launch with progressive accumulation (PATHTRACE frames): d_accum holds
+ * 3 int64 fixed-point sums per pixel of the earlier samples (zeroed to start);
+ * the launch adds this frame's samples and writes the mean over accum_spp (the
+ * samples in d_accum afterwards).  NULL d_accum = wo_dev_launch. */
+int wo_dev_launch_ex(WoDev* dev, WoFrame const* frame, void* d_out, void* stream,
+                     unsigned long long* d_segments, long long* d_accum, uint32_t accum_spp, char* err,
+                     size_t errlen);
+/* Progressive accumulation buffer for a width x height frame (3 int64 per
+ * pixel), zeroed (async, on the device stream) when `reset` or reallocated. */
+int wo_dev_accum_prepare(WoDev* dev, uint32_t width, uint32_t height, int reset, long long** d_accum, char* err,
+                         size_t errlen);
+/* The draw_frame pipeline: render a whole frame into frame slot 0 or 1 (with
+ * accumulation when d_accum), copy it to the slot's pinned host buffer and
+ * record the slot's event -- all asynchronous on the device stream. */
+int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, long long* d_accum, uint32_t accum_spp,
+                        char* err, size_t errlen);
+/* Wait for the slot's frame; *host = its pixels (RGBA float, valid until the
+ * slot is submitted again). */
+int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, char* err, size_t errlen);
 /* Full frame into host memory (synchronous; owns a device frame buffer). */
 int wo_dev_render_host(WoDev* dev, WoFrame const* frame, float* host_rgba, char* err, size_t errlen);
 /* Un-interleave gathered rank buffers into a frame (async on `stream`). */

@@ -70,9 +70,22 @@ struct Wo_Renderer {
     int jit_loaded;     /* the device runs the scene-specialised kernel */
     int lanes_loaded;   /* the device runs the lane-traversal kernel */
 
-    float* host_frame;
-    size_t host_frame_cap;
     uint64_t frames_drawn;
+    uint64_t view_version;  /* bumped by every scene / material / camera change */
+
+    /* progressive accumulation (draw_frame when `progressive`, render_accumulate) */
+    int progressive;
+    int acc_valid;
+    uint32_t acc_spp;          /* samples per pixel in the accumulation */
+    Wo_RenderParams acc_params;
+    uint64_t acc_view;
+
+    /* draw_frame pipeline: frame k renders while frame k-1 is presented */
+    int pending[2];
+    uint32_t pend_w[2], pend_h[2];
+    uint64_t frame_seq;
+    float const* last_frame;
+    uint32_t last_w, last_h;
 };
 
 /* scene_compile.c */

@@ -107,6 +107,11 @@ SIGNATURES = {
     "wo_renderer_render_rows_device": (c_int, [c_void_p, POINTER(RenderParams), c_void_p, c_uint32, c_uint32,
                                                c_uint32, c_void_p, c_void_p]),
     "wo_assemble_rows_device": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_void_p]),
+    "wo_renderer_finish": (c_int, [c_void_p]),
+    "wo_renderer_last_frame": (POINTER(c_float), [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
+    "wo_renderer_set_progressive": (None, [c_void_p, c_int]),
+    "wo_renderer_accumulated_spp": (c_uint32, [c_void_p]),
+    "wo_renderer_render_accumulate": (c_int, [c_void_p, POINTER(RenderParams), c_void_p, c_int]),
     "wo_renderer_compile": (c_int, [c_void_p]),
     "wo_renderer_program": (POINTER(WoRec), [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
     "wo_renderer_materials": (POINTER(WoMaterial), [c_void_p, POINTER(c_uint32)]),
@@ -290,6 +295,42 @@ class Renderer:
         if self.lib.wo_renderer_render_f32(self.ptr, ctypes.byref(params), out.ctypes.data_as(c_void_p)):
             raise WololoError(last_error())
         return out
+
+    def render_accumulate(self, params: RenderParams, reset: bool = False):
+        """params.spp more samples into the progressive accumulation; returns (mean image, total spp)."""
+        import numpy as np
+        out = np.empty((params.height, params.width, 4), dtype=np.float32)
+        n = self.lib.wo_renderer_render_accumulate(self.ptr, ctypes.byref(params), out.ctypes.data_as(c_void_p),
+                                                   1 if reset else 0)
+        if n < 0:
+            raise WololoError(last_error())
+        return out, n
+
+    def draw_frame(self):
+        """wo_renderer_draw_frame (pipelined: presents the previous frame)."""
+        self.lib.wo_renderer_draw_frame(self.ptr)
+
+    def finish(self):
+        if self.lib.wo_renderer_finish(self.ptr):
+            raise WololoError(last_error())
+
+    def last_frame(self):
+        """Copy of the last presented frame (H, W, 4) or None."""
+        import numpy as np
+        w, h = c_uint32(0), c_uint32(0)
+        p = self.lib.wo_renderer_last_frame(self.ptr, ctypes.byref(w), ctypes.byref(h))
+        if not p:
+            return None
+        return np.ctypeslib.as_array(p, shape=(h.value * w.value * 4,)).reshape(h.value, w.value, 4).copy()
+
+    def set_draw_params(self, params: RenderParams, pin_time: bool = True):
+        self.lib.wo_renderer_set_draw_params(self.ptr, ctypes.byref(params), 1 if pin_time else 0)
+
+    def set_progressive(self, on: bool):
+        self.lib.wo_renderer_set_progressive(self.ptr, 1 if on else 0)
+
+    def accumulated_spp(self) -> int:
+        return int(self.lib.wo_renderer_accumulated_spp(self.ptr))
 
     def render_rows_device(self, params: RenderParams, d_out: int, tile_rows: int, rank: int, nranks: int,
                            stream: int = 0, d_segments: int = 0):

@@ -79,6 +79,32 @@ int wo_renderer_render_rows_device(Wo_Renderer* r, Wo_RenderParams const* params
 int wo_assemble_rows_device(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,
                             uint32_t tile_rows, uint32_t nranks, void* stream);
 
+/* ---- frame pipeline and progressive rendering ----
+ * The reference's draw_frame_with_renderer (renderer.c:2085-2219) ends every
+ * frame with vkQueueWaitIdle (2212).  wo_renderer_draw_frame instead submits
+ * frame k (render + copy to pinned host memory, asynchronous) and then waits
+ * for and presents frame k-1: the GPU renders while the host presents, one
+ * frame of latency.  Presenting = the last frame below, plus a PPM dump when
+ * WOLOLO_OUTPUT names a file. */
+/* Wait for and present every submitted frame.  0, or -1 (last_error). */
+int wo_renderer_finish(Wo_Renderer* r);
+/* Host pixels of the last presented frame (RGBA float, row 0 = top; NULL
+ * before the first), valid until the next draw_frame / finish. */
+float const* wo_renderer_last_frame(Wo_Renderer* r, uint32_t* width, uint32_t* height);
+/* Progressive accumulation for draw_frame (off by default): while on,
+ * consecutive PATHTRACE frames with the same scene, camera and draw
+ * parameters add params.spp new samples each (the sample index continues) and
+ * present the mean over all of them -- bit for bit one render of that many
+ * samples.  Any change starts over. */
+void wo_renderer_set_progressive(Wo_Renderer* r, int on);
+/* Samples per pixel in the current accumulation (0: none). */
+uint32_t wo_renderer_accumulated_spp(Wo_Renderer* r);
+/* Synchronous form: render params->spp more samples into the accumulation
+ * (reset != 0, or different parameters / scene: start over) and write the mean
+ * over all accumulated samples to out_rgba (width*height*4 floats, may be
+ * NULL).  Returns the accumulated samples per pixel, or -1. */
+int wo_renderer_render_accumulate(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba, int reset);
+
 /* Compile the node tables into the flattened program (done lazily by every
  * render call; exposed for tests).  Returns the number of records. */
 int wo_renderer_compile(Wo_Renderer* r);

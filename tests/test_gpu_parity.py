@@ -366,3 +366,47 @@ def test_workgroup_tile_shapes(tile, path, monkeypatch):
     ref, _ = _oracle_rows(r, p)
     _cmp(img, ref, f"tile {tile} path={path}")
     r.close()
+
+
+def test_progressive_accumulation_equals_one_render():
+    """k accumulated renders of s samples == one render of k*s samples, bit for bit
+    (exact fixed-point sums carried across launches), from a non-zero sample offset."""
+    r, info = _scene("csg32", "jit")
+    base = info.params(width=72, height=40, spp=3, seed=9, sample_offset=5)
+    img = None
+    for k in range(4):
+        img, n = r.render_accumulate(base, reset=(k == 0))
+        assert n == 3 * (k + 1)
+    full = r.render(info.params(width=72, height=40, spp=12, seed=9, sample_offset=5))
+    _cmp(img, full, "progressive 4 x 3 spp vs 12 spp")
+    ref, _ = _oracle_rows(r, info.params(width=72, height=40, spp=12, seed=9, sample_offset=5))
+    _cmp(img, ref, "progressive vs oracle")
+    r.close()
+
+
+def test_draw_frame_pipeline_and_progressive():
+    """draw_frame keeps one frame in flight and presents in order; with progressive
+    accumulation the presented frame after k draws is the k*spp render; a camera
+    change starts over."""
+    r, info = _scene("csg32", "jit")
+    p = info.params(width=64, height=36, spp=2, seed=4)
+    r.set_draw_params(p)
+    # plain pipeline: every frame is the same render
+    for _ in range(3):
+        r.draw_frame()
+    r.finish()
+    _cmp(r.last_frame(), r.render(p), "pipelined draw_frame")
+    # progressive: 3 draws accumulate 6 samples
+    r.set_progressive(True)
+    for _ in range(3):
+        r.draw_frame()
+    r.finish()
+    assert r.accumulated_spp() == 6
+    _cmp(r.last_frame(), r.render(info.params(width=64, height=36, spp=6, seed=4)), "progressive draw_frame")
+    # a camera change restarts the accumulation
+    r.set_camera((0.0, 4.0, 10.0), (0.0, 0.6, 0.0), (0, 1, 0), 45.0)
+    r.draw_frame()
+    r.finish()
+    assert r.accumulated_spp() == 2
+    _cmp(r.last_frame(), r.render(p), "progressive after a camera change")
+    r.close()
