@@ -295,6 +295,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         const char* v = getenv("WOLOLO_JIT_LDS_PROG");
         if (v && *v) lds_prog = v[0] != '0';
     }
+    /* the register window for deep trees holds 6 events (csg256 chain 29.5 ms at 4,
+     * 27.6 at 6, 27.5 at 8) */
+    if (!g.lds_events) bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW 6\n#endif\n");
     bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
          g.lds_events, tree_depth(prog, n_recs), lds_prog);
     bput(&b, "__constant__ uint32_t kOrdPc[%u] = {", n_prims ? n_prims : 1u);
