@@ -62,6 +62,7 @@ typedef struct Ctx {
     int failed;
     int bound_min_leaves; /* smallest subtree (in leaves) that gets a BOUND record */
     int regroup_unions;   /* rebuild union clusters as a BVH (WOLOLO_REGROUP_UNIONS=0: keep the scene's) */
+    int bvh_sah;          /* split by surface-area cost (WOLOLO_BVH_SAH=0: at the median) */
 } Ctx;
 
 #define MAX_EXPANDED_NODES (1u << 21)
@@ -479,7 +480,33 @@ static int union_of(Ctx* c, int l, int r) {
     return id;
 }
 
-static int bvh_build(Ctx* c, int* ids, int n, SortKey* tmp) {
+/* Running box of operand bounding spheres; its surface area. */
+typedef struct Box3 {
+    double lo[3], hi[3];
+} Box3;
+static void box_reset(Box3* b) {
+    for (int k = 0; k < 3; ++k) {
+        b->lo[k] = INFINITY;
+        b->hi[k] = -INFINITY;
+    }
+}
+static void box_add(Box3* b, const ENode* e) {
+    for (int k = 0; k < 3; ++k) {
+        if (e->bc[k] - e->br < b->lo[k]) b->lo[k] = e->bc[k] - e->br;
+        if (e->bc[k] + e->br > b->hi[k]) b->hi[k] = e->bc[k] + e->br;
+    }
+}
+static double box_area(const Box3* b) {
+    const double x = b->hi[0] - b->lo[0], y = b->hi[1] - b->lo[1], z = b->hi[2] - b->lo[2];
+    return 2.0 * (x * y + y * z + z * x);
+}
+
+/* Sort along the longest centre axis, then split where the surface-area cost
+ * (box area x operands, both sides) is least; clusters of < 16 operands split
+ * at the median.  Measured (1080p64): rtiow_cover 32.4 -> 30.3 ms, csg256 balanced
+ * 15.7 -> 15.4 with the area split; csg32's 11-operand cluster is better at
+ * the median (5.29 vs 5.35). */
+static int bvh_build(Ctx* c, int* ids, int n, SortKey* tmp, int sah) {
     if (n == 1) return ids[0];
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = 0; i < n; ++i)
@@ -498,8 +525,31 @@ static int bvh_build(Ctx* c, int* ids, int n, SortKey* tmp) {
     qsort(tmp, (size_t)n, sizeof(SortKey), cmp_sortkey);
     for (int i = 0; i < n; ++i) ids[i] = tmp[i].id;
     int h = n / 2;
-    int l = bvh_build(c, ids, h, tmp);
-    int r = bvh_build(c, ids + h, n - h, tmp);
+    if (sah && n > 4) {
+        /* prefix areas left to right in tmp[].key, then sweep from the right */
+        double* left = (double*)malloc(sizeof(double) * (size_t)n);
+        if (left) {
+            Box3 bx;
+            box_reset(&bx);
+            for (int i = 1; i < n; ++i) {
+                box_add(&bx, &c->e[ids[i - 1]]);
+                left[i] = box_area(&bx) * i;
+            }
+            box_reset(&bx);
+            double best = INFINITY;
+            for (int i = n - 1; i >= 1; --i) {
+                box_add(&bx, &c->e[ids[i]]);
+                double cost = left[i] + box_area(&bx) * (n - i);
+                if (cost < best) {
+                    best = cost;
+                    h = i;
+                }
+            }
+            free(left);
+        }
+    }
+    int l = bvh_build(c, ids, h, tmp, sah);
+    int r = bvh_build(c, ids + h, n - h, tmp, sah);
     if (l < 0 || r < 0) return -1;
     return union_of(c, l, r);
 }
@@ -563,8 +613,30 @@ static int regroup(Ctx* c, int id) {
         fail(c, "out of host memory");
         return -1;
     }
-    int root = nb ? bvh_build(c, ops, nb, tmp) : -1;
-    for (int i = nb; i < n && !c->failed; ++i) root = root < 0 ? ops[i] : union_of(c, root, ops[i]);
+    /* Giant operands (bounding radius > 16x the cluster's median, e.g. an RTIOW
+     * ground sphere of radius 1000) would give every BOUND above them a giant
+     * sphere that no ray misses: they join the unbounded operands on top. */
+    if (nb > 2) {
+        for (int i = 0; i < nb; ++i) {
+            tmp[i].key = c->e[ops[i]].br;
+            tmp[i].id = ops[i];
+        }
+        qsort(tmp, (size_t)nb, sizeof(SortKey), cmp_sortkey);
+        const double lim = 16.0 * tmp[nb / 2].key;
+        int k = 0;
+        for (int i = 0; i < nb; ++i)
+            if (!(c->e[ops[i]].br > lim)) tmp[k++].id = ops[i];
+        int kept = k;
+        for (int i = 0; i < nb; ++i)
+            if (c->e[ops[i]].br > lim) tmp[k++].id = ops[i];
+        for (int i = 0; i < nb; ++i) ops[i] = tmp[i].id;
+        nb = kept;
+    }
+    int root = nb ? bvh_build(c, ops, nb, tmp, c->bvh_sah && nb >= 16) : -1;
+    /* giant and unbounded operands go first in the program (postfix order), so a
+     * traversal meets a ground plane or sphere -- the likely nearest hit of a
+     * downward ray -- before the hierarchy it may then prune */
+    for (int i = nb; i < n && !c->failed; ++i) root = root < 0 ? ops[i] : union_of(c, ops[i], root);
     free(tmp);
     free(ops);
     return c->failed ? -1 : root;
@@ -692,6 +764,11 @@ int wo_compile_scene(Wo_Renderer* r, char* err, size_t errlen) {
     c.errlen = errlen;
     c.bound_min_leaves = 2;
     c.regroup_unions = 1;
+    c.bvh_sah = 1;
+    {
+        const char* v = getenv("WOLOLO_BVH_SAH");
+        if (v && strcmp(v, "0") == 0) c.bvh_sah = 0;
+    }
     {
         const char* v = getenv("WOLOLO_REGROUP_UNIONS");
         if (v && strcmp(v, "0") == 0) c.regroup_unions = 0;
