@@ -34,8 +34,8 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scene", default="csg32",
                     choices=["csg32", "rtiow_cover", "csg256_balanced", "csg256_chain", "csg32_union", "csg256_balanced_union",
                              "sphere256"])
