@@ -9,8 +9,8 @@
  *   - leaf parameters become fp32 literals (no LDS/global reads, no VGPRs);
  *   - BOUND culling becomes a scalar branch around the subtree's code, its
  *     ballot result kept in an SGPR for the later evaluations;
- *   - the CSG evaluation becomes straight-line bit operations on named values
- *     (1 VALU per node) instead of a decoded postfix walk.
+ *   - the CSG evaluation becomes straight-line masked compares of the membership
+ *     words (one per literal set, gen_eval_flat) instead of a decoded postfix walk.
  * The arithmetic, event order and tie-breaking are exactly the interpreter's
  * (wo_device_common.h), so both paths agree bit-for-bit with the oracle.
  */
@@ -86,6 +86,7 @@ typedef struct Gen {
     uint32_t nbound;  /* BOUND counter (cull flag names) */
     int first_pass;   /* gen_collect: the first pass (cull tests, bits at t_min) or a re-collect */
     uint32_t nval;    /* value counter (eval temporaries) */
+    int flat_eval;    /* gen_eval_flat: literal sets tested with one mask compare */
     int err;
 } Gen;
 
@@ -229,6 +230,146 @@ static uint32_t gen_eval(Gen* g, uint32_t start, uint32_t end, int indent) {
     return stack[0];
 }
 
+/* ---- eval, flattened: literal sets as one masked compare ----
+ * A conjunction of primitive literals (x and not-y terms, primitives of one bits
+ * word) is true iff (bits & (P|N)) == P; a disjunction iff (bits & (P|N)) != N.
+ * Unions / intersections / differences of such sets merge into one set, so a
+ * union of k primitives costs one AND and one compare instead of 2k-1 bit ops;
+ * the remaining combinations are bools, which the compiler keeps as wave lane
+ * masks (SALU).  Same function of `bits` as gen_eval. */
+typedef struct Term {
+    /* kind 0: the named bool v; kind 1: v & conj(P, N); kind 2: v | disj(P, N),
+     * v == kNoName meaning the literal set alone (an empty set is the identity) */
+    int kind;
+    uint32_t w, P, N, v;
+} Term;
+
+enum { kNoName = 0xffffffffu };
+
+static int term_is_literal(const Term* t) {
+    uint32_t m = t->P | t->N;
+    return t->kind && t->v == kNoName && m && (m & (m - 1u)) == 0u;
+}
+
+/* the literal set of t (kind 1/2) as a named bool */
+static uint32_t lits_name(Gen* g, const Term* t, int indent) {
+    uint32_t v = g->nval++;
+    bput(g->b, "%*sconst bool v%u = (bits[%u] & 0x%08xu) %s 0x%08xu;\n", indent, "", v, t->w, t->P | t->N,
+         t->kind == 1 ? "==" : "!=", t->kind == 1 ? t->P : t->N);
+    return v;
+}
+
+static uint32_t bool_op(Gen* g, uint32_t x, uint32_t y, int kind, int indent) {
+    if (x == kNoName) return y;
+    if (y == kNoName) return x;
+    uint32_t v = g->nval++;
+    bput(g->b, "%*sconst bool v%u = v%u %s v%u;\n", indent, "", v, x, kind == 1 ? "&" : "|", y);
+    return v;
+}
+
+static uint32_t term_name(Gen* g, const Term* t, int indent) {
+    if (t->kind == 0) return t->v;
+    if ((t->P | t->N) == 0u) {
+        if (t->v != kNoName) return t->v;
+        uint32_t v = g->nval++;
+        bput(g->b, "%*sconst bool v%u = %s;\n", indent, "", v, t->kind == 1 ? "true" : "false");
+        return v;
+    }
+    return bool_op(g, t->v, lits_name(g, t, indent), t->kind, indent);
+}
+
+/* not(v & C) = !v | not C; not(v | D) = !v & not D */
+static Term term_not(Gen* g, Term t, int indent) {
+    uint32_t nv = kNoName;
+    if (t.v != kNoName) {
+        nv = g->nval++;
+        bput(g->b, "%*sconst bool v%u = !v%u;\n", indent, "", nv, t.v);
+    }
+    if (t.kind == 0) {
+        Term r = {0, 0, 0, 0, nv};
+        return r;
+    }
+    Term r = {t.kind == 1 ? 2 : 1, t.w, t.N, t.P, nv};
+    return r;
+}
+
+/* kind 1: intersection, kind 2: union.  Literal sets of one bits word merge. */
+static Term term_join(Gen* g, Term a, Term b, int kind, int indent) {
+    Term x[2] = {a, b};
+    for (int i = 0; i < 2; ++i) {
+        if (x[i].kind == kind) continue;
+        if (term_is_literal(&x[i])) {
+            x[i].kind = kind;
+            continue;
+        }
+        uint32_t v = term_name(g, &x[i], indent);
+        Term n = {kind, 0, 0, 0, v};
+        x[i] = n;
+    }
+    Term r = {kind, x[0].w, x[0].P, x[0].N, kNoName};
+    uint32_t m0 = x[0].P | x[0].N, m1 = x[1].P | x[1].N;
+    uint32_t extra = kNoName;
+    if (!m0) {
+        r.w = x[1].w, r.P = x[1].P, r.N = x[1].N;
+    } else if (m1 && (x[1].w != x[0].w || (m0 & m1))) {
+        extra = lits_name(g, &x[1], indent);
+    } else {
+        r.P |= x[1].P, r.N |= x[1].N;
+    }
+    r.v = bool_op(g, bool_op(g, x[0].v, x[1].v, kind, indent), extra, kind, indent);
+    return r;
+}
+
+static Term gen_eval_flat(Gen* g, uint32_t start, uint32_t end, int indent) {
+    Term stack[64], none = {0, 0, 0, 0, 0};
+    int sp = 0;
+    uint32_t pc = start;
+    while (pc < end && !g->err) {
+        const WoRec* r = &g->prog[pc];
+        if (sp >= 64) {
+            g->err = 1;
+            return none;
+        }
+        if (r->op == WO_OP_BOUND && r->u1 < g->bound_min_leaves) {
+            ++pc;
+        } else if (r->op == WO_OP_BOUND) {
+            uint32_t k = g->nbound++;
+            Term t = {0, 0, 0, 0, g->nval++};
+            bput(g->b, "%*sbool v%u = false;\n%*sif (!(cull[%u] & %uu)) {\n", indent, "", t.v, indent, "", k / 32,
+                 1u << (k % 32));
+            Term inner = gen_eval_flat(g, pc + 1, r->u0, indent + 2);
+            uint32_t iv = term_name(g, &inner, indent + 2);
+            bput(g->b, "%*s  v%u = v%u;\n%*s}\n", indent, "", t.v, iv, indent, "");
+            stack[sp++] = t;
+            pc = r->u0;
+        } else if (r->op == WO_OP_PRIM) {
+            Term t = {1, r->u1 / 32u, 1u << (r->u1 % 32u), 0u, kNoName};
+            stack[sp++] = t;
+            pc += 1 + r->u0;
+        } else {
+            if (sp < 2) {
+                g->err = 1;
+                return none;
+            }
+            Term B = stack[--sp], A = stack[--sp];
+            if (r->op == WO_OP_UNION)
+                stack[sp++] = term_join(g, A, B, 2, indent);
+            else if (r->op == WO_OP_INTER)
+                stack[sp++] = term_join(g, A, B, 1, indent);
+            else if (r->op == WO_OP_DIFF)
+                stack[sp++] = term_join(g, A, term_not(g, B, indent), 1, indent);
+            else /* RDIFF: B & ~A */
+                stack[sp++] = term_join(g, B, term_not(g, A, indent), 1, indent);
+            ++pc;
+        }
+    }
+    if (sp != 1) {
+        g->err = 1;
+        return none;
+    }
+    return stack[0];
+}
+
 /* Depth of the CSG tree over primitives (a primitive is depth 0). */
 static uint32_t tree_depth(const WoRec* prog, uint32_t n_recs) {
     uint32_t stack[256];
@@ -277,6 +418,11 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     {
         const char* v = getenv("WOLOLO_JIT_LDS_EVENTS");
         if (v && *v) g.lds_events = v[0] != '0';
+    }
+    g.flat_eval = 1;
+    {
+        const char* v = getenv("WOLOLO_JIT_FLAT_EVAL");
+        if (v && *v) g.flat_eval = v[0] != '0';
     }
     uint32_t nbounds = 0;
     for (uint32_t i = 0; i < n_recs; ++i) nbounds += prog[i].op == WO_OP_BOUND && prog[i].u1 >= g.bound_min_leaves;
@@ -350,8 +496,14 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "      uint32_t r;\n"
              "      {\n");
         g.nbound = 0;
-        uint32_t rv = gen_eval(&g, 0, n_recs, 8);
-        bput(&b, "        r = v%u;\n      }\n", rv);
+        if (g.flat_eval) {
+            Term rt = gen_eval_flat(&g, 0, n_recs, 8);
+            uint32_t rv = term_name(&g, &rt, 8);
+            bput(&b, "        r = v%u ? 1u : 0u;\n      }\n", rv);
+        } else {
+            uint32_t rv = gen_eval(&g, 0, n_recs, 8);
+            bput(&b, "        r = v%u;\n      }\n", rv);
+        }
         bput(&b,
              "      if (have && r != root) { wodev::hit_from_key(key, r, hit); return true; }\n"
              "      root = r;\n"
