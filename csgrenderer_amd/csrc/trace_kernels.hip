@@ -899,18 +899,22 @@ extern "C" double wo_dev_jit_compile_sec(WoDev* dev) { return dev ? dev->jit_com
 // the frame while the last big tiles finish.  Measured (csg32 1080p64, slowest
 // rank, tools/rank_share.py): no tail 5.57 / 2.87 / 1.60 / 1.09 ms at N = 1 / 2 /
 // 4 / 8 (8x8 tiles throughout); 3-round tail 5.50 / 2.81 / 1.53 / 0.81 ms.  The big shape is 8x8
-// unless the frame is too small for that to fill the device once; `resident` =
-// workgroups the device holds at once.  Env (measurements): WOLOLO_TILE=8x8|8x4|4x4
-// forces one shape everywhere; WOLOLO_TILE_TAIL=<rounds> sets the tail (0: none).
+// while the frame holds >= 8 rounds of such tiles, else 8x4 (2-round tail), else 4x4
+// (plan_tiles); `resident` = workgroups the device holds at once.  Env (measurements):
+// WOLOLO_TILE=8x8|8x4|4x4 forces one shape everywhere (plus a tail only when
+// WOLOLO_TILE_TAIL is set); WOLOLO_TILE_TAIL=<rounds> sets the tail (0: none).
+// "WxH" with W, H in {1, 2, 4, 8} and W*H <= kTileMaxPix; 0 if not such a shape
 static uint32_t shape_of(const char* f) {
-    if (!strcmp(f, "8x8")) return 3u | (3u << 4);
-    if (!strcmp(f, "8x4")) return 3u | (2u << 4);
-    if (!strcmp(f, "4x4")) return 2u | (2u << 4);
-    return 0u;
+    unsigned w = 0, h = 0;
+    if (sscanf(f, "%ux%u", &w, &h) != 2) return 0u;
+    auto lg = [](unsigned v) -> int { return v == 1u ? 0 : v == 2u ? 1 : v == 4u ? 2 : v == 8u ? 3 : -1; };
+    const int lw = lg(w), lh = lg(h);
+    if (lw < 0 || lh < 0 || w * h > kTileMaxPix) return 0u;
+    return (uint32_t)lw | ((uint32_t)lh << 4);
 }
 static uint32_t tiles_across(uint32_t width, uint32_t shape) { return (width + (1u << (shape & 15u)) - 1u) >> (shape & 15u); }
 
-static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident) {
+static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, uint32_t band_rows) {
     const uint32_t s44 = 2u | (2u << 4);
     PathLaunch g = {};
     g.small_log2 = s44;
@@ -921,11 +925,23 @@ static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident) {
     const char* f = getenv("WOLOLO_TILE");
     uint32_t big = (f && *f) ? shape_of(f) : 0u;
     if (big) {
-        tail_rounds = 0.0;
+        if (!(tv && *tv)) tail_rounds = 0.0;  // a forced shape covers the frame unless a tail is asked for
     } else {
+        // The largest shape that gives every resident workgroup >= 8 tiles: a
+        // workgroup's tiles then average out the costly ones (glass, deep CSG),
+        // which otherwise set the end of a short launch.  8x8 keeps a 3-round
+        // tail of 4x4 tiles, 8x4 a 2-round one.  Measured (tools/rank_share.py,
+        // 1080p64, slowest rank of 4 / 8, ms): csg32 8x8 1.454 / 0.770, 8x4 1.400 /
+        // 0.762, 4x4 1.499 / 0.786; csg256 balanced 8x4 4.73 / 3.50, 4x4 4.23 / 2.34;
+        // csg256 chain 8x4 7.34 / 5.02, 4x4 7.99 / 4.15; rtiow 8x4 8.47 / 4.30,
+        // 4x4 8.27 / 4.37.  One GPU keeps 8x8 (csg32 5.18 vs 5.37 ms at 8x4).
+        const uint64_t want_tiles = 8ull * resident;
         big = 3u | (3u << 4);
-        if ((uint64_t)tiles_across(width, big) * (rows >> 3) < resident) big = 3u | (2u << 4);
-        if ((uint64_t)tiles_across(width, big) * (rows >> 2) < resident) big = s44;
+        if ((uint64_t)tiles_across(width, big) * (rows >> 3) < want_tiles || band_rows < 8u) {
+            big = 3u | (2u << 4);
+            if (!(tv && *tv)) tail_rounds = 2.0;
+        }
+        if ((uint64_t)tiles_across(width, big) * (rows >> 2) < want_tiles) big = s44;
     }
     g.big_log2 = big;
     g.tiles_x_big = tiles_across(width, big);
@@ -1044,7 +1060,10 @@ extern "C" int wo_dev_launch_ex(WoDev* dev, WoFrame const* frame_in, void* d_out
             break;
         }
         if (e != hipSuccess || per_cu < 1) per_cu = 1;
-        PathLaunch tg = plan_tiles(fr.width, local_rows, (uint32_t)dev->cus * (uint32_t)per_cu);
+        // a rank's local rows are bands of tile_rows consecutive frame rows: a tile
+        // taller than a band would join rows far apart (incoherent primary rays)
+        PathLaunch tg = plan_tiles(fr.width, local_rows, (uint32_t)dev->cus * (uint32_t)per_cu,
+                                   fr.nranks > 1u ? fr.tile_rows : ~0u);
         if (d_accum && fr.mode == WO_MODE_PATHTRACE) {
             tg.acc = d_accum;
             tg.acc_spp = accum_spp;
