@@ -444,6 +444,10 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     /* the register window for deep trees holds 6 events (csg256 chain 29.5 ms at 4,
      * 27.6 at 6, 27.5 at 8) */
     if (!g.lds_events) bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW 6\n#endif\n");
+    /* small scenes run 8 waves per SIMD: a 7-entry LDS list keeps 8 workgroups'
+     * LDS within the CU (csg32 5.24 -> 5.19 ms; csg256 balanced keeps 8 entries:
+     * 15.12 vs 15.33 ms at 7) */
+    if (g.lds_events && n_prims <= 64u) bput(&b, "#ifndef WO_LDS_EVENTS\n#define WO_LDS_EVENTS 7\n#endif\n");
     bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
          g.lds_events, tree_depth(prog, n_recs), lds_prog);
     bput(&b, "__constant__ uint32_t kOrdPc[%u] = {", n_prims ? n_prims : 1u);
@@ -531,12 +535,13 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "};\n");
     }
     /* Waves per SIMD the register budget is sized for (measured, 1920x1080x64):
-     * csg32 (18 primitives) 6.62 ms at 6, 6.50 at 7, 6.65 at 8; csg256 balanced /
-     * chain (128) 23.7 / 38.0 ms at 6, 21.3 / 33.8 at 8. */
+     * csg256 balanced / chain (128 primitives) 23.7 / 38.0 ms at 6, 21.3 / 33.8 at
+     * 8; csg32 (18) 5.24 ms at 7 (8 LDS events), 5.19 at 8 (7 LDS events: 8
+     * workgroups' LDS fit the CU only then). */
     bput(&b,
          "\n#ifndef WO_JIT_MIN_WAVES\n"
          "#define WO_JIT_MIN_WAVES %u\n#endif\n",
-         n_prims > 64u ? 8u : 7u);
+         (n_prims > 64u || g.lds_events) ? 8u : 7u);
     bput(&b,
          "extern \"C\" __global__ __launch_bounds__(256, WO_JIT_MIN_WAVES) void wo_jit_pathtrace(\n"
          "    const WoRec* __restrict__ prog, const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t local_rows,\n"

@@ -335,7 +335,7 @@ def test_auto_tracer_choices():
         r.close()
 
 
-@pytest.mark.parametrize("window", ["lds2", "lds8", "registers"])
+@pytest.mark.parametrize("window", ["lds2", "lds", "registers"])
 def test_jit_event_windows(window, monkeypatch):
     """The specialised kernel's two event windows (LDS list, register window) and
     the LDS list's overflow barrier (capacity 2 forces it on most rays that meet
