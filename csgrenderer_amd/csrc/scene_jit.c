@@ -403,8 +403,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     g.b = &b;
     uint32_t nw = n_prims ? (n_prims + 31u) / 32u : 1u;
     /* Wave-level BOUND tests pay only for larger subtrees (measured: csg32 6.54 ms
-     * testing subtrees of >= 8 leaves vs 6.94 ms testing every BOUND record). */
-    g.bound_min_leaves = 8;
+     * testing subtrees of >= 8 leaves vs 6.94 ms testing every BOUND record; with
+     * the later kernel 5.17 ms at >= 8, 5.11 at >= 6, 5.13 at >= 5, 5.30 at >= 12). */
+    g.bound_min_leaves = 6;
     {
         const char* v = getenv("WOLOLO_JIT_BOUND_MIN_LEAVES");
         if (v && *v) g.bound_min_leaves = (uint32_t)strtoul(v, NULL, 10);
