@@ -87,6 +87,7 @@ typedef struct Gen {
     int first_pass;   /* gen_collect: the first pass (cull tests, bits at t_min) or a re-collect */
     uint32_t nval;    /* value counter (eval temporaries) */
     int flat_eval;    /* gen_eval_flat: literal sets tested with one mask compare */
+    int axis_pairs;   /* consecutive opposite faces on one axis fused (axis_pair_meet) */
     int err;
 } Gen;
 
@@ -125,6 +126,21 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
                 uint32_t vl[4];
                 for (int i = 0; i < 4; ++i) vl[i] = fbits(L->f[i]);
                 bput(g->b, "%*s  {\n", indent, "");
+                const WoRec* L2 = m + 1u < cnt ? &g->prog[pc + 2 + m] : NULL;
+                if (g->axis_pairs && L->op == WO_LEAF_HALFSPACE && L->u1 != 0u && L2 && L2->op == WO_LEAF_HALFSPACE &&
+                    L2->u1 == L->u1 && (L->f[L->u1 - 1u] > 0.0f) != (L2->f[L2->u1 - 1u] > 0.0f)) {
+                    /* two faces of a slab: one entry, one exit (axis_pair_meet) */
+                    static const char* nh[2] = {"c3", "c3b"};
+                    static const char axis[3] = {'x', 'y', 'z'};
+                    const char ax = axis[L->u1 - 1u];
+                    uint32_t vh[2] = {vl[3], fbits(L2->f[3])};
+                    emit_consts(g->b, indent + 4, "float", nh, vh, 2);
+                    if (m == 0) bput(g->b, "%*s    wodev::ivl_open(iv);\n", indent, "");
+                    bput(g->b, "%*s    wodev::axis_pair_meet(iv, %s, c3, c3b, o.%c, d.%c, iv%c, %uu, %uu);\n%*s  }\n",
+                         indent, "", L->f[L->u1 - 1u] > 0.0f ? "1.0f" : "-1.0f", ax, ax, ax, m, m + 1u, indent, "");
+                    ++m;
+                    continue;
+                }
                 if (L->op == WO_LEAF_HALFSPACE && L->u1 != 0u) {
                     /* axis-aligned: s = +-1 stays a literal (inline constant), h in an SGPR */
                     static const char* nh[1] = {"c3"};
@@ -419,6 +435,11 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     {
         const char* v = getenv("WOLOLO_JIT_LDS_EVENTS");
         if (v && *v) g.lds_events = v[0] != '0';
+    }
+    g.axis_pairs = 1;
+    {
+        const char* v = getenv("WOLOLO_JIT_AXIS_PAIRS");
+        if (v && *v) g.axis_pairs = v[0] != '0';
     }
     g.flat_eval = 1;
     {

@@ -266,6 +266,47 @@ def test_edge_scenes(path):
     r.close()
 
 
+def _axis_center_dir(fr):
+    """The normals-mode ray direction of the centre pixel, as the kernels compute it (fp32)."""
+    f32 = np.float32
+    c = fr.cam
+    x, y = fr.width // 2, fr.height // 2
+    sx = f32(f32(x) + f32(0.5)) * f32(fr.inv_width)
+    ty = f32(f32(fr.height - 1 - y) + f32(0.5)) * f32(fr.inv_height)
+    return [f32(f32(f32(c.lower_left[i]) + sx * f32(c.horizontal[i])) + ty * f32(c.vertical[i])) - f32(c.origin[i])
+            for i in range(3)]
+
+
+@pytest.mark.parametrize("path", ["jit", "interpreter"])
+def test_axis_parallel_rays_through_slabs(path):
+    """Rays parallel to box faces (a direction component exactly 0): the specialised
+    kernel's fused slab-pair path falls back to the per-face form there.  The centre
+    pixel looks straight down -z, the centre row has d.y = 0, and a fuzz-free mirror
+    face sends rays straight back along +z."""
+    r = wl.Renderer("slabs", max_nodes=64)
+    r.set_tracer(path)
+    front, front_planes = scenes._box_extents(r, (0.0, 0.0, -3.0), (0.5, 0.5, 0.5))
+    back, _ = scenes._box_extents(r, (0.0, 0.0, 4.0), (2.0, 2.0, 0.5))
+    side, side_planes = scenes._box_extents(r, (1.5, 0.0, -5.0), (0.5, 1.0, 0.5))
+    u = r.union(wl.arg(front), wl.arg(back))
+    r.union(wl.arg(u), wl.arg(side))
+    mirror, clay = r.metal((0.9, 0.9, 0.9), 0.0), r.lambertian((0.2, 0.6, 0.3))
+    for pl in front_planes:
+        r.set_material(pl, mirror)
+    for pl in side_planes:
+        r.set_material(pl, clay)
+    r.set_camera((0, 0, 0), (0, 0, -1), (0, 1, 0), 60.0, 0.0, 1.0)
+    for mode, spp in [(wl.MODE_NORMALS, 1), (wl.MODE_PATHTRACE, 4)]:
+        p = wl.render_params(33, 33, spp=spp, max_depth=4, mode=mode, seed=3)
+        if mode == wl.MODE_NORMALS:
+            dx, dy, dz = _axis_center_dir(r.frame_desc(p))
+            assert dx == 0.0 and dy == 0.0 and dz < 0.0, (dx, dy, dz)
+        img = r.render(p)
+        ref, _ = _oracle_rows(r, p)
+        _cmp(img, ref, f"slabs mode={mode} path={path}")
+    r.close()
+
+
 def test_draw_frame_demo_path():
     """The reference's demo flow (main.c:38-51): new, add nodes, isroot, draw."""
     r = wl.Renderer("Test1Render", max_nodes=8)

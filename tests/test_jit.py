@@ -15,16 +15,20 @@ def test_csg32_source_compiles_for_gfx950(hostonly):
     prog, nrec, nprim = r.program()
     src = r.jit_source()
     assert src is not None
-    # one intersection call per leaf in each of the two collect passes (first pass,
-    # re-collect), one cull flag per BOUND, ordinal table of every primitive
+    # one intersection call per leaf (a slab's two opposite faces: one pair call) in
+    # each of the two collect passes (first pass, re-collect), one cull flag per
+    # BOUND, ordinal table of every primitive
     nleaf = sum(1 for i in range(nrec) if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE))
-    assert len(re.findall(r"wodev::(sphere|halfspace|halfspace_axis)_interval\(", src)) == 2 * nleaf
+    nsingle = len(re.findall(r"wodev::(sphere|halfspace|halfspace_axis)_interval\(", src))
+    npair = len(re.findall(r"wodev::axis_pair_meet\(", src))
+    assert npair >= 2 * 6  # the slab and the cube: three face pairs each, in both passes
+    assert nsingle + 2 * npair == 2 * nleaf
     # the slab and the cube are axis-aligned: tagged by the compiler, emitted on the fast path
     naxis = sum(1 for i in range(nrec) if prog[i].op == wl.WO_LEAF_HALFSPACE and prog[i].u1 != 0)
     assert naxis >= 12
-    assert len(re.findall(r"wodev::halfspace_axis_interval\(", src)) == 2 * naxis
-    # wave-level tests only for BOUND subtrees of >= 8 leaves (scene_jit.c, WOLOLO_JIT_BOUND_MIN_LEAVES)
-    nb = sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND and prog[i].u1 >= 8)
+    assert len(re.findall(r"wodev::halfspace_axis_interval\(", src)) + 2 * npair == 2 * naxis
+    # wave-level tests only for BOUND subtrees of >= 6 leaves (scene_jit.c, WOLOLO_JIT_BOUND_MIN_LEAVES)
+    nb = sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND and prog[i].u1 >= 6)
     assert 0 < nb < sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND)
     assert len(re.findall(r"if \(__ballot\(wodev::bound_may_hit\(", src)) == nb
     m = re.search(r"kOrdPc\[(\d+)\] = \{([^}]*)\}", src)
