@@ -420,7 +420,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     uint32_t nw = n_prims ? (n_prims + 31u) / 32u : 1u;
     /* Wave-level BOUND tests pay only for larger subtrees (measured: csg32 6.54 ms
      * testing subtrees of >= 8 leaves vs 6.94 ms testing every BOUND record; with
-     * the later kernel 5.17 ms at >= 8, 5.11 at >= 6, 5.13 at >= 5, 5.30 at >= 12). */
+     * the later kernel 5.17 ms at >= 8, 5.11 at >= 6, 5.13 at >= 5, 5.30 at >= 12; with fused slab
+     * faces 4.93 at >= 6, 4.95 at 4 / 5, 4.98 at 7, 4.99 at 8; csg256 balanced 15.0 at 6, 15.2 at 4 / 8). */
     g.bound_min_leaves = 6;
     {
         const char* v = getenv("WOLOLO_JIT_BOUND_MIN_LEAVES");
