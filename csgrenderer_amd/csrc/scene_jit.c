@@ -88,6 +88,7 @@ typedef struct Gen {
     uint32_t nval;    /* value counter (eval temporaries) */
     int flat_eval;    /* gen_eval_flat: literal sets tested with one mask compare */
     int axis_pairs;   /* consecutive opposite faces on one axis fused (axis_pair_meet) */
+    int member_skip;  /* members after the first skipped when the interval is empty on every lane */
     int err;
 } Gen;
 
@@ -121,10 +122,13 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
             static const char* nk[2] = {"ka", "kb"};
             bput(g->b, "%*s{  // primitive %u (%u leaves)\n", indent, "", ord, cnt);
             bput(g->b, "%*s  wodev::Ivl iv; float la, lb;\n", indent, "");
+            int open_skips = 0;
             for (uint32_t m = 0; m < cnt; ++m) {
                 const WoRec* L = &g->prog[pc + 1 + m];
                 uint32_t vl[4];
                 for (int i = 0; i < 4; ++i) vl[i] = fbits(L->f[i]);
+                if (m > 0 && g->member_skip) /* empty on every lane: the other members cannot widen it */
+                    bput(g->b, "%*s  if (__ballot(!(iv.a > iv.b)) != 0ull) {\n", indent, ""), ++open_skips;
                 bput(g->b, "%*s  {\n", indent, "");
                 const WoRec* L2 = m + 1u < cnt ? &g->prog[pc + 2 + m] : NULL;
                 if (g->axis_pairs && L->op == WO_LEAF_HALFSPACE && L->u1 != 0u && L2 && L2->op == WO_LEAF_HALFSPACE &&
@@ -162,6 +166,7 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
                     bput(g->b, "%*s    wodev::ivl_meet(iv, la, lb, %uu);\n", indent, "", m);
                 bput(g->b, "%*s  }\n", indent, "");
             }
+            for (; open_skips > 0; --open_skips) bput(g->b, "%*s  }\n", indent, "");
             uint32_t vk[2] = {ord << 12, (ord << 12) | (1u << 11)};
             bput(g->b, "%*s  if (!(iv.a > iv.b)) {\n", indent, "");
             emit_consts(g->b, indent + 4, "uint32_t", nk, vk, 2);
@@ -441,6 +446,11 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     {
         const char* v = getenv("WOLOLO_JIT_AXIS_PAIRS");
         if (v && *v) g.axis_pairs = v[0] != '0';
+    }
+    g.member_skip = 1;
+    {
+        const char* v = getenv("WOLOLO_JIT_MEMBER_SKIP");
+        if (v && *v) g.member_skip = v[0] != '0';
     }
     g.flat_eval = 1;
     {

@@ -64,3 +64,21 @@ def test_empty_scene_has_no_source(hostonly):
     r = wl.Renderer("e", max_nodes=2)
     assert r.jit_source() is None
     r.close()
+
+
+def test_member_skip_guards(hostonly, monkeypatch):
+    """Members after a primitive's first are guarded by a wave-level emptiness test
+    (scene_jit.c member_skip): one guard per later member in each collect pass, none
+    with WOLOLO_JIT_MEMBER_SKIP=0.  Exact: a met interval only narrows."""
+    guard = "if (__ballot(!(iv.a > iv.b)) != 0ull)"
+    r = wl.Renderer("skip", max_nodes=4096)
+    scenes.build("csg32", r)
+    prog, nrec, _ = r.program()
+    src = r.jit_source()
+    pair_members = len(re.findall(r"wodev::axis_pair_meet\(", src))  # a pair is one member step
+    singles = len(re.findall(r"wodev::(sphere|halfspace|halfspace_axis)_interval\(", src))
+    nprims_emitted = 2 * sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_PRIM)
+    assert src.count(guard) == singles + pair_members - nprims_emitted > 0
+    monkeypatch.setenv("WOLOLO_JIT_MEMBER_SKIP", "0")
+    assert guard not in r.jit_source()
+    r.close()
