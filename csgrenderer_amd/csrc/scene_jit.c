@@ -88,16 +88,29 @@ typedef struct Gen {
     uint32_t nval;    /* value counter (eval temporaries) */
     int flat_eval;    /* gen_eval_flat: literal sets tested with one mask compare */
     int axis_pairs;   /* consecutive opposite faces on one axis fused (axis_pair_meet) */
+    int bound_single; /* BOUND records around a single primitive tested too */
     int member_skip;  /* members after the first skipped when the interval is empty on every lane */
     int err;
 } Gen;
+
+/* A BOUND record gets a wave-level test when its subtree has enough leaves, and
+ * (bound_single off) when it holds more than one primitive: a lone convex
+ * primitive's own first member, with the member skip, is the cheaper test. */
+static int bound_tested(const Gen* g, uint32_t pc) {
+    const WoRec* r = &g->prog[pc];
+    if (r->u1 < g->bound_min_leaves) return 0;
+    if (!g->bound_single && pc + 1u < g->n && g->prog[pc + 1u].op == WO_OP_PRIM &&
+        pc + 2u + g->prog[pc + 1u].u0 == r->u0)
+        return 0;
+    return 1;
+}
 
 /* ---- collect: intersect every primitive of [start, end), fill the window ---- */
 static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
     uint32_t pc = start;
     while (pc < end && !g->err) {
         const WoRec* r = &g->prog[pc];
-        if (r->op == WO_OP_BOUND && r->u1 < g->bound_min_leaves) {
+        if (r->op == WO_OP_BOUND && !bound_tested(g, pc)) {
             ++pc; /* too small to pay for a wave-level test: the subtree is emitted inline */
         } else if (r->op == WO_OP_BOUND) {
             static const char* nb[5] = {"bc0", "bc1", "bc2", "bc3", "bc4"};
@@ -200,7 +213,7 @@ static uint32_t gen_eval(Gen* g, uint32_t start, uint32_t end, int indent) {
     uint32_t pc = start;
     while (pc < end && !g->err) {
         const WoRec* r = &g->prog[pc];
-        if (r->op == WO_OP_BOUND && r->u1 < g->bound_min_leaves) {
+        if (r->op == WO_OP_BOUND && !bound_tested(g, pc)) {
             ++pc;
         } else if (r->op == WO_OP_BOUND) {
             uint32_t k = g->nbound++;
@@ -351,7 +364,7 @@ static Term gen_eval_flat(Gen* g, uint32_t start, uint32_t end, int indent) {
             g->err = 1;
             return none;
         }
-        if (r->op == WO_OP_BOUND && r->u1 < g->bound_min_leaves) {
+        if (r->op == WO_OP_BOUND && !bound_tested(g, pc)) {
             ++pc;
         } else if (r->op == WO_OP_BOUND) {
             uint32_t k = g->nbound++;
@@ -458,7 +471,14 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         if (v && *v) g.flat_eval = v[0] != '0';
     }
     uint32_t nbounds = 0;
-    for (uint32_t i = 0; i < n_recs; ++i) nbounds += prog[i].op == WO_OP_BOUND && prog[i].u1 >= g.bound_min_leaves;
+    /* with the member skip, a bound around one convex primitive costs more than it
+     * saves (csg32 4.87 / 4.87 ms with it, 4.83 / 4.82 without, same box) */
+    g.bound_single = 0;
+    {
+        const char* v = getenv("WOLOLO_JIT_BOUND_SINGLE");
+        if (v && *v) g.bound_single = v[0] != '0';
+    }
+    for (uint32_t i = 0; i < n_recs; ++i) nbounds += prog[i].op == WO_OP_BOUND && bound_tested(&g, i);
 
     bput(&b, "// generated by scene_jit.c: %u records, %u primitives, %u bounds\n", n_recs, n_prims, nbounds);
     /* Small programs are copied to LDS per workgroup with the materials they use:
