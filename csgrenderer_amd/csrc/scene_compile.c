@@ -63,6 +63,7 @@ typedef struct Ctx {
     int bound_min_leaves; /* smallest subtree (in leaves) that gets a BOUND record */
     int regroup_unions;   /* rebuild union clusters as a BVH (WOLOLO_REGROUP_UNIONS=0: keep the scene's) */
     int bvh_sah;          /* split by surface-area cost (WOLOLO_BVH_SAH=0: at the median) */
+    int small_spheres_first; /* convex members: spheres by ascending radius (WOLOLO_MEMBER_ORDER=0: scene order) */
 } Ctx;
 
 #define MAX_EXPANDED_NODES (1u << 21)
@@ -732,6 +733,24 @@ static void emit(Ctx* c, int id, double outer_r) {
             free(mem);
             return;
         }
+        if (c->small_spheres_first) {
+            /* the sphere members in ascending radius (stable; half-spaces keep their
+             * slots, so slab face pairs stay adjacent): the kernels skip a primitive's
+             * later members once its interval is empty on a whole wave, and the
+             * smallest sphere empties it most often */
+            for (int i = 1; i < cnt; ++i) {
+                if (c->e[mem[i]].kind != E_SPHERE) continue;
+                for (int j = i; j > 0;) {
+                    int k = j - 1;
+                    while (k >= 0 && c->e[mem[k]].kind != E_SPHERE) --k;
+                    if (k < 0 || !(c->e[mem[j]].rad < c->e[mem[k]].rad)) break;
+                    int t = mem[j];
+                    mem[j] = mem[k];
+                    mem[k] = t;
+                    j = k;
+                }
+            }
+        }
         p->op = WO_OP_PRIM;
         p->u0 = (uint32_t)cnt;
         p->u1 = c->ordinal++;
@@ -765,6 +784,11 @@ int wo_compile_scene(Wo_Renderer* r, char* err, size_t errlen) {
     c.bound_min_leaves = 2;
     c.regroup_unions = 1;
     c.bvh_sah = 1;
+    c.small_spheres_first = 1;
+    {
+        const char* v = getenv("WOLOLO_MEMBER_ORDER");
+        if (v && *v) c.small_spheres_first = v[0] != '0';
+    }
     {
         const char* v = getenv("WOLOLO_BVH_SAH");
         if (v && strcmp(v, "0") == 0) c.bvh_sah = 0;
