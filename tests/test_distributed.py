@@ -90,7 +90,7 @@ def test_row_tiles_gather_assemble(tmp_path, monkeypatch, world):
     r.close()
 
 
-@pytest.mark.parametrize("height,tile,n", [(1080, 16, 1), (1080, 16, 8), (2160, 16, 8), (37, 8, 3), (5, 16, 4)])
+@pytest.mark.parametrize("height,tile,n", [(1080, 16, 1), (1080, 16, 8), (2160, 16, 8), (1080, 4, 8), (2160, 4, 8), (1080, 4, 7), (37, 8, 3), (5, 16, 4)])
 def test_partition_covers_every_row_once(height, tile, n):
     from csgrenderer_amd import wololo as wl
     lr = wl.local_rows(height, tile, n)
