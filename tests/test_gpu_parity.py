@@ -394,6 +394,31 @@ def test_jit_event_windows(window, monkeypatch):
         r.close()
 
 
+@pytest.mark.parametrize("knobs", [
+    {"WOLOLO_JIT_MEMBER_SKIP": "0", "WOLOLO_JIT_BOUND_SINGLE": "1"},
+    {"WOLOLO_JIT_MEMBER_SKIP": "1", "WOLOLO_JIT_BOUND_SINGLE": "1"},
+    {"WOLOLO_MEMBER_ORDER": "0"},
+    {"WOLOLO_JIT_FLAGS": "-DWO_LDS_NEXT_EAGER=0"},
+    {"WOLOLO_JIT_FLAGS": "-DWO_LDS_NEXT_EAGER=7"},
+])
+def test_jit_culling_knobs(knobs, monkeypatch):
+    """The wave-level member skip, the bound-around-a-lone-primitive rule, the
+    scene compiler's sphere-member order and the sweep's eager event reads change
+    how much work a wave does, never the image: every setting gives the oracle's
+    frame on the scenes with multi-member primitives (csg32's lenses and rounded
+    cube, csg256 balanced's 21 sphere intersections)."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    for name in ["csg32", "csg256_balanced"]:
+        r, info = _scene(name, "jit")
+        p = info.params(width=64, height=36, spp=4, seed=13)
+        img = r.render(p)
+        _check_path(r, "jit")
+        ref, _ = _oracle_rows(r, p)
+        _cmp(img, ref, f"{name} {knobs}")
+        r.close()
+
+
 @pytest.mark.parametrize("tile", ["8x8", "8x4", "4x4"])
 @pytest.mark.parametrize("path", PATHS)
 def test_workgroup_tile_shapes(tile, path, monkeypatch):
