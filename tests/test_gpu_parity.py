@@ -400,6 +400,7 @@ def test_jit_event_windows(window, monkeypatch):
     {"WOLOLO_MEMBER_ORDER": "0"},
     {"WOLOLO_JIT_FLAGS": "-DWO_LDS_NEXT_EAGER=0"},
     {"WOLOLO_JIT_FLAGS": "-DWO_LDS_NEXT_EAGER=7"},
+    {"WOLOLO_JIT_FLAGS": "-DWO_LDS_EVENTS=2 -DWO_LDS_NEXT_EAGER=7"},  # eager reads clamped to the list
 ])
 def test_jit_culling_knobs(knobs, monkeypatch):
     """The wave-level member skip, the bound-around-a-lone-primitive rule, the
