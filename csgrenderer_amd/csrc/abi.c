@@ -1,0 +1,54 @@
+/*
+ * abi.c -- the C compiler's view of the value types that cross the C ABI
+ * (renderer.h, renderer_ext.h, wo_scene.h), so bindings in other languages can
+ * check their mirrors field by field (tests/test_api.py checks the ctypes ones
+ * in csgrenderer_amd/wololo.py).  The reference passes Wo_Node_Argument by
+ * value (renderer.h:22-33); a mirror with a wrong field offset corrupts every
+ * binop silently, so the check is worth an exported symbol.
+ */
+#include <stddef.h>
+#include <string.h>
+
+#include "wololo/renderer/renderer_ext.h"
+#include "wololo/wo_scene.h"
+
+typedef struct AbiField {
+    const char* type;
+    const char* field; /* NULL: the type's size */
+    size_t value;
+} AbiField;
+
+#define T(ty) {#ty, NULL, sizeof(ty)}
+#define F(ty, fl) {#ty, #fl, offsetof(ty, fl)}
+
+static const AbiField kAbi[] = {
+    T(Wo_Vec3), F(Wo_Vec3, x), F(Wo_Vec3, y), F(Wo_Vec3, z),
+    T(Wo_Quaternion), F(Wo_Quaternion, real), F(Wo_Quaternion, imaginary),
+    T(Wo_Node_Argument), F(Wo_Node_Argument, orientation), F(Wo_Node_Argument, offset), F(Wo_Node_Argument, node),
+    T(Wo_RenderParams), F(Wo_RenderParams, width), F(Wo_RenderParams, height), F(Wo_RenderParams, spp),
+    F(Wo_RenderParams, max_depth), F(Wo_RenderParams, seed), F(Wo_RenderParams, mode),
+    F(Wo_RenderParams, sample_offset), F(Wo_RenderParams, time_sec),
+    T(WoRec), F(WoRec, op), F(WoRec, u0), F(WoRec, u1), F(WoRec, f),
+    T(WoMaterial), F(WoMaterial, kind), F(WoMaterial, albedo), F(WoMaterial, fuzz), F(WoMaterial, ior),
+    F(WoMaterial, inv_ior), F(WoMaterial, r0),
+    T(WoCamera), F(WoCamera, origin), F(WoCamera, lower_left), F(WoCamera, horizontal), F(WoCamera, vertical),
+    F(WoCamera, u), F(WoCamera, v), F(WoCamera, lens_radius), F(WoCamera, pad),
+    T(WoFrame), F(WoFrame, width), F(WoFrame, height), F(WoFrame, spp), F(WoFrame, max_depth), F(WoFrame, seed),
+    F(WoFrame, mode), F(WoFrame, sample_offset), F(WoFrame, tile_rows), F(WoFrame, rank), F(WoFrame, nranks),
+    F(WoFrame, n_recs), F(WoFrame, n_prims), F(WoFrame, time_sec), F(WoFrame, sphere_y), F(WoFrame, inv_width),
+    F(WoFrame, inv_height), F(WoFrame, cam),
+};
+
+#undef T
+#undef F
+
+size_t wo_abi_layout(char const* type, char const* field) {
+    if (!type) return (size_t)-1;
+    for (size_t i = 0; i < sizeof kAbi / sizeof kAbi[0]; ++i) {
+        const AbiField* a = &kAbi[i];
+        if (strcmp(a->type, type) != 0) continue;
+        if (!field && !a->field) return a->value;
+        if (field && a->field && strcmp(a->field, field) == 0) return a->value;
+    }
+    return (size_t)-1;
+}

@@ -30,6 +30,8 @@ void wo_set_error(char const* fmt, ...) {
 
 char const* wo_renderer_last_error(void) { return g_err; }
 
+void wo_renderer_clear_error(void) { g_err[0] = '\0'; }
+
 char const* wo_version(void) { return "wololo-mi355x 0.1 (gfx950)"; }
 
 double wo_monotonic_sec(void) {
@@ -362,6 +364,12 @@ static int sync_device(Wo_Renderer* r) {
     if (wo_renderer_compile(r) < 0) return -1;
     if (r->dev_stale) {
         char err[256] = {0};
+        /* The pipeline may still hold a frame of the old scene on the device
+         * stream (draw_frame returns with one in flight): retire it first, so it
+         * is presented in order and finishes before its program, traversal table
+         * and kernel module are replaced.  wo_dev_upload_scene then drains every
+         * other stream of the device (render_rows_device on a caller's stream). */
+        if (wo_renderer_finish(r)) return -1;
         if (wo_dev_upload_scene(r->dev, r->prog, r->n_recs, r->n_prims, r->mats, r->n_mats, err, sizeof err)) {
             wo_set_error("scene upload failed: %s", err);
             return -1;
@@ -459,57 +467,32 @@ int wo_assemble_rows_device(void const* d_gathered, void* d_frame, uint32_t widt
 
 /* ---------------------------------------------------------------- draw_frame */
 
-/* Present path, headless: the float framebuffer is clamped, sRGB-encoded (the
- * reference's preferred B8G8R8A8_SRGB swapchain, renderer.c:819-831) and, when
- * WOLOLO_OUTPUT names a file, written as a binary PPM. */
-static unsigned char srgb8(float v) {
-    if (!(v > 0.0f)) return 0;
-    if (v >= 1.0f) return 255;
-    float s = v <= 0.0031308f ? 12.92f * v : 1.055f * powf(v, 1.0f / 2.4f) - 0.055f;
-    int q = (int)(s * 255.0f + 0.5f);
-    return (unsigned char)(q < 0 ? 0 : q > 255 ? 255 : q);
-}
-
-static void write_ppm(const char* path, const float* rgba, uint32_t w, uint32_t h) {
-    FILE* f = fopen(path, "wb");
-    if (!f) {
-        fprintf(stderr, WO_LOG_PREFIX " cannot write %s\n", path);
-        return;
-    }
-    fprintf(f, "P6\n%u %u\n255\n", w, h);
-    unsigned char* row = (unsigned char*)malloc((size_t)w * 3);
-    if (row) {
-        for (uint32_t y = 0; y < h; ++y) {
-            for (uint32_t x = 0; x < w; ++x)
-                for (int c = 0; c < 3; ++c) row[x * 3 + c] = srgb8(rgba[((size_t)y * w + x) * 4 + c]);
-            fwrite(row, 1, (size_t)w * 3, f);
-        }
-        free(row);
-    }
-    fclose(f);
-}
-
-/* Present a finished frame: keep it as the last frame and dump it when
- * WOLOLO_OUTPUT names a file (the headless stand-in for the swapchain). */
-static void present(Wo_Renderer* r, float const* px, uint32_t w, uint32_t h) {
+/* Present a finished frame: keep it (float and its B8G8R8A8 sRGB encode, made
+ * on the GPU: present.c) as the last frame, and dump it as a binary PPM when
+ * WOLOLO_OUTPUT names a file (the headless stand-in for the swapchain,
+ * ref renderer.c:2160-2211). */
+static void present(Wo_Renderer* r, float const* px, uint32_t const* bgra8, uint32_t w, uint32_t h) {
     r->last_frame = px;
+    r->last_bgra8 = bgra8;
     r->last_w = w;
     r->last_h = h;
     r->frames_drawn++;
     const char* out = getenv("WOLOLO_OUTPUT");
-    if (out && *out) write_ppm(out, px, w, h);
+    if (out && *out && bgra8 && wo_write_ppm_bgra8(out, bgra8, w, h))
+        fprintf(stderr, WO_LOG_PREFIX " present: %s\n", wo_renderer_last_error());
 }
 
 static int retire_slot(Wo_Renderer* r, int slot) {
     if (!r->pending[slot]) return 0;
     char err[256] = {0};
     float const* px = NULL;
+    uint32_t const* bgra8 = NULL;
     r->pending[slot] = 0;
-    if (wo_dev_frame_wait(r->dev, slot, &px, err, sizeof err)) {
+    if (wo_dev_frame_wait(r->dev, slot, &px, &bgra8, err, sizeof err)) {
         wo_set_error("frame wait failed: %s", err);
         return -1;
     }
-    present(r, px, r->pend_w[slot], r->pend_h[slot]);
+    present(r, px, bgra8, r->pend_w[slot], r->pend_h[slot]);
     return 0;
 }
 
@@ -601,6 +584,21 @@ float const* wo_renderer_last_frame(Wo_Renderer* r, uint32_t* width, uint32_t* h
     return r->last_frame;
 }
 
+uint32_t const* wo_renderer_last_frame_bgra8(Wo_Renderer* r, uint32_t* width, uint32_t* height) {
+    if (width) *width = r->last_bgra8 ? r->last_w : 0u;
+    if (height) *height = r->last_bgra8 ? r->last_h : 0u;
+    return r->last_bgra8;
+}
+
+int wo_srgb8_encode_device(void const* d_rgba, void* d_bgra8, size_t pixels, void* stream) {
+    char err[256] = {0};
+    if (wo_dev_srgb8(d_rgba, d_bgra8, pixels, stream, err, sizeof err)) {
+        wo_set_error("%s", err);
+        return -1;
+    }
+    return 0;
+}
+
 int wo_renderer_render_accumulate(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba, int reset) {
     if (params->mode != WO_SHADING_PATHTRACE) {
         wo_set_error("render_accumulate needs WO_SHADING_PATHTRACE");
@@ -612,7 +610,7 @@ int wo_renderer_render_accumulate(Wo_Renderer* r, Wo_RenderParams const* params,
     r->pending[0] = 0;
     char err[256] = {0};
     float const* px = NULL;
-    if (wo_dev_frame_wait(r->dev, 0, &px, err, sizeof err)) {
+    if (wo_dev_frame_wait(r->dev, 0, &px, NULL, err, sizeof err)) {
         wo_set_error("frame wait failed: %s", err);
         return -1;
     }

@@ -68,6 +68,10 @@ typedef struct Ctx {
 
 #define MAX_EXPANDED_NODES (1u << 21)
 #define MAX_GROUP_MEMBERS 2047u
+/* expand, analyse, regroup and emit recurse once per tree level (a few hundred
+ * bytes of native stack each): 8192 levels stay within ~3 MB, so a user-built
+ * chain fails with an error instead of overflowing the thread's stack */
+#define MAX_TREE_DEPTH 8192
 
 static void fail(Ctx* c, const char* msg) {
     if (!c->failed) snprintf(c->err, c->errlen, "%s", msg);
@@ -149,8 +153,8 @@ static int expand(Ctx* c, Wo_Node node, const Xf* xf, int depth) {
         fail(c, "binop operand refers to a node that does not exist");
         return -1;
     }
-    if (depth > 100000) {
-        fail(c, "scene graph too deep");
+    if (depth > MAX_TREE_DEPTH) {
+        fail(c, "scene graph too deep (more than 8192 nested binops)");
         return -1;
     }
     const WoNodeInfo* ni = &r->nodes[node];
@@ -241,7 +245,8 @@ static void cross3d(const double a[3], const double b[3], double o[3]) {
 
 /* Bounding sphere of the polytope {x : n_i.x <= h_i}; returns 0 if unbounded/empty. */
 static int polytope_bound(const double (*n)[3], const double* h, int k, double oc[3], double* orad) {
-    if (k < 4) return 0;
+    /* O(k^4): callers pass at most 64 planes; more are treated as unbounded */
+    if (k < 4 || k > 64) return 0;
     int any_pair = 0;
     for (int i = 0; i < k; ++i)
         for (int j = i + 1; j < k; ++j) {
@@ -260,7 +265,8 @@ static int polytope_bound(const double (*n)[3], const double* h, int k, double o
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     int nv = 0;
     /* vertices: every independent triple of planes, kept if it satisfies all constraints */
-    double* verts = (double*)malloc(sizeof(double) * 3 * (size_t)(k * k * k / 6 + 8));
+    const size_t kk = (size_t)k;
+    double* verts = (double*)malloc(sizeof(double) * 3 * (kk * kk * kk / 6 + 8));
     if (!verts) return 0;
     for (int a = 0; a < k; ++a)
         for (int b = a + 1; b < k; ++b)

@@ -533,6 +533,34 @@ __global__ __launch_bounds__(kBlock) void assemble_kernel(const float4* __restri
     }
 }
 
+// Present encode (present.c): float RGBA -> B8G8R8A8 sRGB, the reference's
+// preferred swapchain format (renderer.c:813-832).  A channel's code is the
+// count of the 255 thresholds <= its value (binary search in LDS), which is
+// round-half-up(255 * srgb(clamp(v))) exactly; NaN -> 0.  HBM-bound: 16 B read
+// + 4 B written per pixel.
+__device__ __forceinline__ uint32_t srgb8_code(const float* t, float v) {
+    uint32_t k = 0;
+#pragma unroll
+    for (uint32_t s = 128u; s > 0u; s >>= 1)
+        if (t[k + s - 1u] <= v) k += s;  // t[255] = +inf keeps k <= 255
+    return k;
+}
+__device__ __forceinline__ uint32_t unorm8(float a) {
+    if (!(a > 0.0f)) return 0u;
+    if (a >= 1.0f) return 255u;
+    return (uint32_t)(a * 255.0f + 0.5f);
+}
+__global__ __launch_bounds__(kBlock) void srgb8_kernel(const float4* __restrict__ in, uint32_t* __restrict__ out,
+                                                       size_t n, const float* __restrict__ tab) {
+    __shared__ float t[256];
+    t[threadIdx.x] = threadIdx.x < 255u ? tab[threadIdx.x] : kInf;
+    __syncthreads();
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock) {
+        const float4 p = in[i];
+        out[i] = srgb8_code(t, p.z) | (srgb8_code(t, p.y) << 8) | (srgb8_code(t, p.x) << 16) | (unorm8(p.w) << 24);
+    }
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -565,6 +593,10 @@ struct WoDev {
     size_t dslot_cap[2];
     float* h_slot[2];
     size_t hslot_cap[2];
+    uint32_t* d_bgra[2];  // the slot's frame encoded for present (B8G8R8A8 sRGB)
+    size_t dbgra_cap[2];
+    uint32_t* h_bgra[2];
+    size_t hbgra_cap[2];
     hipEvent_t slot_ev[2];
     bool union_only;
     bool lanes_on;
@@ -636,6 +668,8 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
         if (dev->d_slot[i]) (void)hipFree(dev->d_slot[i]);
         if (dev->h_slot[i]) (void)hipHostFree(dev->h_slot[i]);
         if (dev->slot_ev[i]) (void)hipEventDestroy(dev->slot_ev[i]);
+        if (dev->d_bgra[i]) (void)hipFree(dev->d_bgra[i]);
+        if (dev->h_bgra[i]) (void)hipHostFree(dev->h_bgra[i]);
     }
     if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
     (void)hipStreamDestroy(dev->stream);
@@ -745,6 +779,15 @@ extern "C" int wo_dev_upload_scene(WoDev* dev, WoRec const* prog, uint32_t n_rec
     hipError_t e = hipSetDevice(dev->device);
     if (e != hipSuccess) {
         set_err(err, errlen, "hipSetDevice", e);
+        return -1;
+    }
+    // Kernels of the previous scene may still run on any stream of the device
+    // (the frame pipeline's, or a caller's stream for render_rows_device): the
+    // buffers below are overwritten (or reallocated) in place and the JIT module
+    // replaced next, so the whole device drains first.  Scene changes are rare.
+    e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipDeviceSynchronize (before scene upload)", e);
         return -1;
     }
     if (ensure_buffer(&dev->d_prog, &dev->prog_cap, (size_t)n_recs * sizeof(WoRec), err, errlen)) return -1;
@@ -1211,11 +1254,31 @@ extern "C" int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, l
             return -1;
         }
     }
+    if (pixels * sizeof(uint32_t) > dev->hbgra_cap[slot] || !dev->h_bgra[slot]) {
+        if (dev->h_bgra[slot]) (void)hipHostFree(dev->h_bgra[slot]);
+        dev->h_bgra[slot] = nullptr;
+        dev->hbgra_cap[slot] = 0;
+        e = hipHostMalloc((void**)&dev->h_bgra[slot], pixels ? pixels * sizeof(uint32_t) : 64, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            dev->h_bgra[slot] = nullptr;
+            set_err(err, errlen, "hipHostMalloc(present slot)", e);
+            return -1;
+        }
+        dev->hbgra_cap[slot] = pixels * sizeof(uint32_t);
+    }
+    if (ensure_buffer(&dev->d_bgra[slot], &dev->dbgra_cap[slot], pixels * sizeof(uint32_t), err, errlen)) return -1;
     if (wo_dev_launch_ex(dev, &fr, dev->d_slot[slot], dev->stream, nullptr, d_accum, accum_spp, err, errlen))
         return -1;
     if (pixels) {
+        // the float frame (wo_renderer_last_frame) and its present encode
+        // (wo_renderer_last_frame_bgra8): whole frame, one rank, so the local
+        // rows are the frame rows
+        if (wo_dev_srgb8(dev->d_slot[slot], dev->d_bgra[slot], pixels, dev->stream, err, errlen)) return -1;
         e = hipMemcpyAsync(dev->h_slot[slot], dev->d_slot[slot], pixels * sizeof(float4), hipMemcpyDeviceToHost,
                            dev->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(dev->h_bgra[slot], dev->d_bgra[slot], pixels * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, dev->stream);
         if (e != hipSuccess) {
             set_err(err, errlen, "hipMemcpyAsync(frame slot)", e);
             return -1;
@@ -1229,7 +1292,8 @@ extern "C" int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, l
     return 0;
 }
 
-extern "C" int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, char* err, size_t errlen) {
+extern "C" int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, uint32_t const** host_bgra8, char* err,
+                                 size_t errlen) {
     if (slot < 0 || slot > 1 || !dev->slot_ev[slot]) {
         snprintf(err, errlen, "frame slot %d was never submitted", slot);
         return -1;
@@ -1240,6 +1304,50 @@ extern "C" int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, char*
         return -1;
     }
     *host = dev->h_slot[slot];
+    if (host_bgra8) *host_bgra8 = dev->h_bgra[slot];
+    return 0;
+}
+
+// The present encode's threshold table, one copy per device (built once).
+static std::mutex g_srgb_mu;
+static float* g_srgb_tab[64];
+
+extern "C" int wo_dev_srgb8(void const* d_rgba, void* d_bgra8, size_t pixels, void* stream, char* err,
+                            size_t errlen) {
+    if (pixels == 0) return 0;
+    int d = -1;
+    hipError_t e = hipGetDevice(&d);
+    if (e != hipSuccess || d < 0 || d >= 64) {
+        set_err(err, errlen, "hipGetDevice", e);
+        return -1;
+    }
+    float* tab = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_srgb_mu);
+        if (!g_srgb_tab[d]) {
+            float host[255];
+            wo_srgb8_thresholds(host);
+            float* p = nullptr;
+            e = hipMalloc((void**)&p, sizeof host);
+            if (e == hipSuccess) e = hipMemcpy(p, host, sizeof host, hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                if (p) (void)hipFree(p);
+                set_err(err, errlen, "sRGB table upload", e);
+                return -1;
+            }
+            g_srgb_tab[d] = p;
+        }
+        tab = g_srgb_tab[d];
+    }
+    size_t blocks = (pixels + kBlock - 1) / kBlock;
+    if (blocks > 16384u) blocks = 16384u;
+    hipLaunchKernelGGL(srgb8_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream,
+                       (const float4*)d_rgba, (uint32_t*)d_bgra8, pixels, (const float*)tab);
+    e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_err(err, errlen, "sRGB encode launch", e);
+        return -1;
+    }
     return 0;
 }
 

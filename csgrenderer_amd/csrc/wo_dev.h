@@ -52,13 +52,20 @@ int wo_dev_launch_ex(WoDev* dev, WoFrame const* frame, void* d_out, void* stream
 int wo_dev_accum_prepare(WoDev* dev, uint32_t width, uint32_t height, int reset, long long** d_accum, char* err,
                          size_t errlen);
 /* The draw_frame pipeline: render a whole frame into frame slot 0 or 1 (with
- * accumulation when d_accum), copy it to the slot's pinned host buffer and
- * record the slot's event -- all asynchronous on the device stream. */
+ * accumulation when d_accum), encode it for present (sRGB, B8G8R8A8), copy both
+ * to the slot's pinned host buffers and record the slot's event -- all
+ * asynchronous on the device stream. */
 int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, long long* d_accum, uint32_t accum_spp,
                         char* err, size_t errlen);
-/* Wait for the slot's frame; *host = its pixels (RGBA float, valid until the
- * slot is submitted again). */
-int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, char* err, size_t errlen);
+/* Wait for the slot's frame; *host = its pixels (RGBA float), *host_bgra8 (if
+ * non-NULL) = its present encode; both valid until the slot is submitted again. */
+int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, uint32_t const** host_bgra8, char* err,
+                      size_t errlen);
+/* Present encode of `pixels` float4 pixels into B8G8R8A8 sRGB (present.c) on
+ * the current device, async on `stream`. */
+int wo_dev_srgb8(void const* d_rgba, void* d_bgra8, size_t pixels, void* stream, char* err, size_t errlen);
+/* present.c: the encode's 255 thresholds (host) */
+void wo_srgb8_thresholds(float out[255]);
 /* Full frame into host memory (synchronous; owns a device frame buffer). */
 int wo_dev_render_host(WoDev* dev, WoFrame const* frame, float* host_rgba, char* err, size_t errlen);
 /* Un-interleave gathered rank buffers into a frame (async on `stream`). */

@@ -85,6 +85,7 @@ struct Wo_Renderer {
     uint32_t pend_w[2], pend_h[2];
     uint64_t frame_seq;
     float const* last_frame;
+    uint32_t const* last_bgra8;  /* its present encode (B8G8R8A8 sRGB) */
     uint32_t last_w, last_h;
 };
 
@@ -94,6 +95,9 @@ void wo_resolve_camera(WoCameraDesc const* desc, uint32_t width, uint32_t height
 
 /* scene_jit.c: HIP source of the scene-specialised trace kernel (malloc'd) */
 char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prims);
+
+/* present.c: binary PPM (RGB) of a B8G8R8A8 frame; 0 or -1 (last_error) */
+int wo_write_ppm_bgra8(char const* path, uint32_t const* bgra8, uint32_t w, uint32_t h);
 
 /* renderer.c */
 void wo_set_error(char const* fmt, ...);

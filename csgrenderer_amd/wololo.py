@@ -109,6 +109,10 @@ SIGNATURES = {
     "wo_assemble_rows_device": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_void_p]),
     "wo_renderer_finish": (c_int, [c_void_p]),
     "wo_renderer_last_frame": (POINTER(c_float), [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
+    "wo_renderer_last_frame_bgra8": (POINTER(c_uint32), [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
+    "wo_srgb8_thresholds": (None, [POINTER(c_float)]),
+    "wo_srgb8_encode_device": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "wo_srgb8_encode_host": (None, [c_void_p, c_void_p, c_size_t]),
     "wo_renderer_set_progressive": (None, [c_void_p, c_int]),
     "wo_renderer_accumulated_spp": (c_uint32, [c_void_p]),
     "wo_renderer_render_accumulate": (c_int, [c_void_p, POINTER(RenderParams), c_void_p, c_int]),
@@ -127,7 +131,9 @@ SIGNATURES = {
     "wo_renderer_name": (c_char_p, [c_void_p]),
     "wo_renderer_device": (c_int, [c_void_p]),
     "wo_renderer_last_error": (c_char_p, []),
+    "wo_renderer_clear_error": (None, []),
     "wo_version": (c_char_p, []),
+    "wo_abi_layout": (c_size_t, [c_char_p, c_char_p]),
     "wo_hip_device_count": (c_int, []),
 }
 
@@ -168,6 +174,10 @@ def arg(node: int, offset=(0.0, 0.0, 0.0), orientation: Quaternion | None = None
 def last_error() -> str:
     e = load().wo_renderer_last_error()
     return e.decode() if e else ""
+
+
+def clear_error():
+    load().wo_renderer_clear_error()
 
 
 class WololoError(RuntimeError):
@@ -323,6 +333,15 @@ class Renderer:
             return None
         return np.ctypeslib.as_array(p, shape=(h.value * w.value * 4,)).reshape(h.value, w.value, 4).copy()
 
+    def last_frame_bgra8(self):
+        """Copy of the last presented frame's present encode, (H, W) uint32 B8G8R8A8 sRGB, or None."""
+        import numpy as np
+        w, h = c_uint32(0), c_uint32(0)
+        p = self.lib.wo_renderer_last_frame_bgra8(self.ptr, ctypes.byref(w), ctypes.byref(h))
+        if not p:
+            return None
+        return np.ctypeslib.as_array(p, shape=(h.value * w.value,)).reshape(h.value, w.value).copy()
+
     def set_draw_params(self, params: RenderParams, pin_time: bool = True):
         self.lib.wo_renderer_set_draw_params(self.ptr, ctypes.byref(params), 1 if pin_time else 0)
 
@@ -351,6 +370,34 @@ def assemble_rows_device(d_gathered: int, d_frame: int, width: int, height: int,
     if lib.wo_assemble_rows_device(c_void_p(d_gathered), c_void_p(d_frame), width, height, tile_rows, nranks,
                                    c_void_p(stream or None)):
         raise WololoError(last_error())
+
+
+def srgb8_thresholds():
+    """The present encode's 255 thresholds (float32 numpy array)."""
+    import numpy as np
+    t = (c_float * 255)()
+    load().wo_srgb8_thresholds(t)
+    return np.frombuffer(t, dtype=np.float32).copy()
+
+
+def srgb8_encode_host(rgba):
+    """(..., 4) float32 RGBA -> (...) uint32 B8G8R8A8 sRGB, the library's host encode."""
+    import numpy as np
+    a = np.ascontiguousarray(rgba, dtype=np.float32)
+    out = np.empty(a.shape[:-1], dtype=np.uint32)
+    load().wo_srgb8_encode_host(a.ctypes.data_as(c_void_p), out.ctypes.data_as(c_void_p), out.size)
+    return out
+
+
+def srgb8_encode_device(d_rgba: int, d_bgra8: int, pixels: int, stream: int = 0):
+    if load().wo_srgb8_encode_device(c_void_p(d_rgba), c_void_p(d_bgra8), pixels, c_void_p(stream or None)):
+        raise WololoError(last_error())
+
+
+def abi_layout(type_name: str, field: str | None = None) -> int:
+    """sizeof / offsetof as the C library was compiled (wo_abi_layout); -1 if unknown."""
+    v = load().wo_abi_layout(type_name.encode(), field.encode() if field else None)
+    return -1 if v == ctypes.c_size_t(-1).value else int(v)
 
 
 def jit_compile_check(src: str, arch: str = "gfx950") -> str:

@@ -91,6 +91,21 @@ int wo_renderer_finish(Wo_Renderer* r);
 /* Host pixels of the last presented frame (RGBA float, row 0 = top; NULL
  * before the first), valid until the next draw_frame / finish. */
 float const* wo_renderer_last_frame(Wo_Renderer* r, uint32_t* width, uint32_t* height);
+/* Present encode of the last presented frame: B8G8R8A8 sRGB, one uint32 per
+ * pixel (B in the low byte) -- the reference's preferred swapchain format
+ * (renderer.c:813-832) -- made on the GPU by wo_srgb8_encode_device.  Same
+ * lifetime as wo_renderer_last_frame. */
+uint32_t const* wo_renderer_last_frame_bgra8(Wo_Renderer* r, uint32_t* width, uint32_t* height);
+/* The sRGB present encode (what the reference's B8G8R8A8_SRGB attachment does in
+ * fixed function): per channel code = round-half-up(255 * srgb(clamp(v, 0, 1)))
+ * with the IEC 61966-2-1 transfer function (NaN -> 0); alpha is linear.
+ * wo_srgb8_thresholds gives the 255 floats the code counts (code(v) = number of
+ * thresholds <= v); the device and host encodes use the same table, so they
+ * agree bit for bit. */
+void wo_srgb8_thresholds(float out[255]);
+int wo_srgb8_encode_device(void const* d_rgba, void* d_bgra8, size_t pixels, void* stream);
+void wo_srgb8_encode_host(float const* rgba, uint32_t* bgra8, size_t pixels);
+
 /* Progressive accumulation for draw_frame (off by default): while on,
  * consecutive PATHTRACE frames with the same scene, camera and draw
  * parameters add params.spp new samples each (the sample index continues) and
@@ -152,8 +167,15 @@ char const* wo_renderer_name(Wo_Renderer* r);
 /* HIP device ordinal the renderer runs on; -1 for a device-less renderer. */
 int wo_renderer_device(Wo_Renderer* r);
 char const* wo_renderer_last_error(void);
+/* Empty this thread's last-error message (so a caller can tell a new failure). */
+void wo_renderer_clear_error(void);
 
 /* ---- library-level ---- */
+/* sizeof(type) (field NULL) or offsetof(type, field) as this library was
+ * compiled, for the value types of the C ABI (Wo_Vec3, Wo_Quaternion,
+ * Wo_Node_Argument, Wo_RenderParams, WoRec, WoMaterial, WoCamera, WoFrame);
+ * (size_t)-1 for an unknown name.  Bindings check their mirrors with it. */
+size_t wo_abi_layout(char const* type, char const* field);
 char const* wo_version(void);
 /* Number of visible HIP devices (0 when none / no driver). */
 int wo_hip_device_count(void);

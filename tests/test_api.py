@@ -5,6 +5,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 from csgrenderer_amd import wololo as wl
@@ -48,10 +49,66 @@ def test_python_mirror_covers_the_abi():
 
 
 def test_abi_sizes():
+    # renderer.h:22-27 (the reference's by-value operand): sizes measured by SURVEY.md 8(b)
     assert ctypes.sizeof(wl.Vec3) == 24
     assert ctypes.sizeof(wl.Quaternion) == 32
     assert ctypes.sizeof(wl.NodeArgument) == 64
-    assert ctypes.sizeof(wl.WoFrame) == 16 * 4 + 22 * 4 + 2 * 4 - 8 or ctypes.sizeof(wl.WoFrame) > 0
+
+
+# C type name -> its ctypes mirror in csgrenderer_amd/wololo.py
+ABI_MIRRORS = {"Wo_Vec3": wl.Vec3, "Wo_Quaternion": wl.Quaternion, "Wo_Node_Argument": wl.NodeArgument,
+               "Wo_RenderParams": wl.RenderParams, "WoRec": wl.WoRec, "WoMaterial": wl.WoMaterial,
+               "WoCamera": wl.WoCamera, "WoFrame": wl.WoFrame}
+
+
+@pytest.mark.parametrize("cname", sorted(ABI_MIRRORS))
+def test_abi_mirror_matches_the_c_layout(cname):
+    """Every field offset and the size of each ctypes mirror equal what the C compiler laid
+    out (wo_abi_layout): a shifted field would corrupt every call that passes the struct."""
+    mirror = ABI_MIRRORS[cname]
+    assert wl.abi_layout(cname) == ctypes.sizeof(mirror), cname
+    for fname, _ in mirror._fields_:
+        if fname == "pad":
+            continue
+        assert wl.abi_layout(cname, fname) == getattr(mirror, fname).offset, (cname, fname)
+    assert wl.abi_layout(cname, "no_such_field") == -1
+    assert wl.abi_layout("NoSuchType") == -1
+
+
+def _srgb_ref(v):
+    """IEC 61966-2-1 encode in float64 and round-half-up to 8 bits (clamped; NaN -> 0)."""
+    v = np.asarray(v, dtype=np.float64)
+    c = np.clip(np.nan_to_num(v, nan=0.0), 0.0, 1.0)
+    s = np.where(c <= 0.0031308, 12.92 * c, 1.055 * np.power(c, 1.0 / 2.4) - 0.055)
+    return np.floor(255.0 * s + 0.5).astype(np.int64), 255.0 * s
+
+
+def srgb_test_values():
+    """Edge values plus a dense sweep of [0, 1] and values either side of every threshold."""
+    t = wl.srgb8_thresholds().astype(np.float32)
+    around = np.concatenate([t, np.nextafter(t, np.float32(-1)), np.nextafter(t, np.float32(2))])
+    edge = np.array([0.0, -0.0, -1.0, 1.0, 2.0, np.inf, -np.inf, np.nan, 1e-45, 0.0031308, 0.04045, 0.5,
+                     np.nextafter(np.float32(1), np.float32(0))], dtype=np.float32)
+    sweep = np.linspace(0.0, 1.0, 200001, dtype=np.float32)
+    return np.concatenate([edge, around.astype(np.float32), sweep])
+
+
+def test_srgb8_thresholds_and_host_encode():
+    """The present encode (renderer.c:813-832 prefers a B8G8R8A8_SRGB swapchain): the table is
+    strictly increasing in (0, 1) and the host encode equals the float64 IEC formula for every
+    tested value except exact ties (none expected)."""
+    t = wl.srgb8_thresholds()
+    assert t.shape == (255,) and np.all(np.diff(t) > 0) and t[0] > 0 and t[-1] < 1
+    v = srgb_test_values()
+    want, x = _srgb_ref(v)
+    tie = np.abs(x - np.floor(x) - 0.5) < 1e-9
+    rgba = np.stack([v, np.roll(v, 1), np.roll(v, 2), np.ones_like(v)], axis=-1)
+    got = wl.srgb8_encode_host(rgba)
+    r, g, b, a = (got >> 16) & 255, (got >> 8) & 255, got & 255, got >> 24
+    ok = ~tie
+    assert np.array_equal(r[ok], want[ok])
+    assert np.array_equal(g, np.roll(r, 1)) and np.array_equal(b, np.roll(r, 2))
+    assert np.all(a == 255)
 
 
 def test_node_store_semantics(hostonly):

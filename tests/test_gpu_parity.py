@@ -5,7 +5,6 @@ IEEE fp32 with the same op order, correctly rounded div/sqrt and no contraction.
 The north_star tolerance (1e-4 max per channel) is asserted as well so a
 failure message shows which bar broke.
 """
-import ctypes
 import json
 import os
 
@@ -127,7 +126,7 @@ def test_pathtrace_small_frame_bitexact(scene, mode, path):
 
 
 @pytest.mark.parametrize("path", PATHS)
-@pytest.mark.parametrize("scene", ["csg32", "rtiow_cover", "csg256_balanced"])
+@pytest.mark.parametrize("scene", ["csg32", "rtiow_cover", "csg256_balanced", "csg256_chain"])
 def test_pathtrace_full_size_sampled_pixels(scene, path):
     """BASELINE configs at full size (1920x1080, 64 spp, 8 bounces): the whole frame on
     the GPU, a random sample of pixels on the oracle."""
@@ -206,6 +205,46 @@ def test_row_tiles_assemble_to_full_frame(nranks, tile, path):
     # segment counter == oracle's count for the whole frame
     _, segs = _oracle_rows(r, p)
     assert int(seg.item()) == segs
+    r.close()
+
+
+def test_c4_csg32_4k_row_tiles_of_8_ranks():
+    """BASELINE config C4 (csg32, 3840x2160, 256 spp, row tiles over 8 GPUs + one gather):
+    the 8 ranks' shares rendered one after another on this GPU, each into its slice of
+    one rank-major buffer (what the gather delivers to rank 0), then un-interleaved.
+    The assembled frame equals one full-frame render bit for bit, 192 sampled pixels
+    equal the oracle's, and the 8 shares' segment counts add up to the full frame's."""
+    torch = _torch()
+    r, info = _scene("csg32", "jit")
+    p = info.params(width=3840, height=2160, spp=256)
+    T, N = 4, 8
+    lr = wl.local_rows(p.height, T, N)
+    stream = torch.cuda.current_stream().cuda_stream
+    full = torch.empty((p.height, p.width, 4), dtype=torch.float32, device="cuda")
+    seg_full = torch.zeros(1, dtype=torch.int64, device="cuda")
+    r.render_rows_device(p, full.data_ptr(), T, 0, 1, stream, seg_full.data_ptr())
+    gathered = torch.zeros((N, lr, p.width, 4), dtype=torch.float32, device="cuda")
+    seg = torch.zeros(N, dtype=torch.int64, device="cuda")
+    for rank in range(N):
+        r.render_rows_device(p, gathered[rank].data_ptr(), T, rank, N, stream, seg[rank:].data_ptr())
+    frame = torch.empty_like(full)
+    wl.assemble_rows_device(gathered.data_ptr(), frame.data_ptr(), p.width, p.height, T, N, stream)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, full), "assembled 8-rank frame differs from the full render"
+    assert int(seg.sum().item()) == int(seg_full.item())
+    # every rank got a share of the work (row-cyclic tiles balance it within a few %)
+    shares = seg.cpu().numpy().astype(np.float64)
+    assert shares.min() > 0.9 * shares.mean(), shares
+    img = full.cpu().numpy()
+    assert np.isfinite(img).all()
+    rng = np.random.default_rng(4321)
+    n = 192
+    xs = rng.integers(0, p.width, n).astype(np.uint32)
+    ys = rng.integers(0, p.height, n).astype(np.uint32)
+    prog, nrec, _ = r.program()
+    mats, nm = r.materials()
+    ref, _ = pyoracle.pathtrace_pixels(prog, nrec, mats, nm, r.frame_desc(p), xs, ys)
+    _cmp(img[ys, xs], ref, "C4 csg32 4K 256spp sampled")
     r.close()
 
 
@@ -304,20 +343,6 @@ def test_axis_parallel_rays_through_slabs(path):
         img = r.render(p)
         ref, _ = _oracle_rows(r, p)
         _cmp(img, ref, f"slabs mode={mode} path={path}")
-    r.close()
-
-
-def test_draw_frame_demo_path():
-    """The reference's demo flow (main.c:38-51): new, add nodes, isroot, draw."""
-    r = wl.Renderer("Test1Render", max_nodes=8)
-    s1 = r.sphere(1.0)
-    s2 = r.sphere(1.0)
-    b = r.union(wl.arg(s1), wl.arg(s2))
-    assert (r.isroot(s1), r.isroot(s2), r.isroot(b)) == (False, False, True)
-    params = wl.render_params(1280, 720, time_sec=0.0)
-    r.lib.wo_renderer_set_draw_params(r.ptr, ctypes.byref(params), 1)
-    r.lib.wo_renderer_draw_frame(r.ptr)
-    assert wl.last_error() == "" or "draw" not in wl.last_error()
     r.close()
 
 

@@ -244,3 +244,20 @@ def test_random_scenes_hits_match_float64_classifier(hostonly, seed, axis):
         res = pyoracle.trace(prog, nrec, o.astype(np.float32).tolist(), d.tolist())
         assert res is not None and res[0] <= dist * (1 + 1e-4) + 1e-4, (seed, p, res)
     r.close()
+
+
+def test_deep_difference_chain_fails_cleanly(hostonly):
+    """A user-built chain deeper than the compiler's recursion limit (8192 levels) is an
+    error, not a native stack overflow; a 4000-deep chain compiles."""
+    for depth, ok in [(4000, True), (9000, False)]:
+        r = wl.Renderer(f"chain{depth}", max_nodes=2 * depth + 4)
+        acc = r.sphere(1.0)
+        for k in range(depth):
+            s = r.sphere(0.1)
+            acc = r.difference(wl.arg(acc), wl.arg(s, (0.0, 0.0, 0.001 * k)))
+        if ok:
+            assert r.compile() > 0
+        else:
+            with pytest.raises(wl.WololoError, match="too deep"):
+                r.compile()
+        r.close()
