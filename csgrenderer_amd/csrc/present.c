@@ -67,7 +67,7 @@ static uint8_t srgb8_code(float v, const float* t) {
 static uint8_t unorm8(float a) {
     if (!(a > 0.0f)) return 0;
     if (a >= 1.0f) return 255;
-    return (uint8_t)(a * 255.0f + 0.5f);
+    return (uint8_t)((double)a * 255.0 + 0.5); /* exact in double: round-half-up */
 }
 
 void wo_srgb8_encode_host(float const* rgba, uint32_t* bgra8, size_t pixels) {

@@ -548,7 +548,7 @@ __device__ __forceinline__ uint32_t srgb8_code(const float* t, float v) {
 __device__ __forceinline__ uint32_t unorm8(float a) {
     if (!(a > 0.0f)) return 0u;
     if (a >= 1.0f) return 255u;
-    return (uint32_t)(a * 255.0f + 0.5f);
+    return (uint32_t)((double)a * 255.0 + 0.5);  // exact in double: round-half-up
 }
 __global__ __launch_bounds__(kBlock) void srgb8_kernel(const float4* __restrict__ in, uint32_t* __restrict__ out,
                                                        size_t n, const float* __restrict__ tab) {
