@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--jit", type=int, default=None, help="legacy: 0 = --tracer interpreter")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo stages the gather through host memory (for rehearsing N>1 ranks on one GPU)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="N>1: gather each frame before the next renders (default: frame k+1 renders while frame k "
+                         "is gathered, with either backend)")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 checks the assembled frame against a single full-frame render (bit-exact)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -99,7 +102,9 @@ def main():
     r.set_tracer("interpreter" if args.jit == 0 else args.tracer)
     W, H, T = params.width, params.height, args.tile_rows
     lr = wl.local_rows(H, T, world)
-    pipelined = world > 1 and not gloo
+    # the same two-buffer / two-stream / event code runs on either backend, so a gloo
+    # rehearsal on one GPU executes what the RCCL run on 8 GPUs does
+    pipelined = world > 1 and not args.no_pipeline
     # two render buffers when pipelined: frame k+1 renders while frame k is gathered
     outs = [torch.empty((lr, W, 4), dtype=torch.float32, device=dev) for _ in range(2 if pipelined else 1)]
     seg = torch.zeros(1, dtype=torch.int64, device=dev)

@@ -135,12 +135,80 @@ Wo_Renderer* wo_renderer_new(Wo_App* app, char const* name, size_t max_node_coun
         return NULL;
     }
     r->device = dev;
+    r->devs[0] = r->dev;
+    r->ndevs = 1;
+    /* Ranks per frame: WOLOLO_DEVICES=N|all, else every visible GPU for a
+     * renderer of the app (the demo's, main.c:38) and one for a library caller
+     * (one process per GPU, e.g. bench.py under torchrun). */
+    int want = 1;
+    const char* dv = getenv("WOLOLO_DEVICES");
+    if (dv && *dv)
+        want = strcmp(dv, "all") == 0 ? ndev : atoi(dv);
+    else if (app)
+        want = ndev;
+    if (want > WO_MAX_DEVICES) want = WO_MAX_DEVICES;
+    if (want > 1 && wo_renderer_set_devices(r, want) < 0)
+        fprintf(stderr, WO_LOG_PREFIX " multi-GPU setup failed (%s); rendering on device %d only.\n",
+                wo_renderer_last_error(), dev);
     return r;
 }
+
+/* Row-cyclic frames over n ranks: rank i on HIP device (device + i) mod
+ * visible devices, so n above the device count stacks ranks on one device
+ * (each rank keeps its own stream and buffers). */
+int wo_renderer_set_devices(Wo_Renderer* r, int n) {
+    if (!r || !r->dev) {
+        wo_set_error("renderer has no HIP device");
+        return -1;
+    }
+    if (n < 1 || n > WO_MAX_DEVICES) {
+        wo_set_error("device count %d out of range [1, %d]", n, WO_MAX_DEVICES);
+        return -1;
+    }
+    if (wo_renderer_finish(r)) return -1;
+    const int ndev = wo_dev_count();
+    const int cur = wo_dev_current();
+    for (uint32_t i = 1; i < r->ndevs; ++i) {
+        wo_dev_destroy(r->devs[i]);
+        r->devs[i] = NULL;
+    }
+    r->ndevs = 1;
+    r->dev_stale = 1; /* every rank needs the scene (and the kernel) */
+    r->acc_valid = 0; /* accumulations are per rank */
+    int rc = n;
+    char err[256] = {0};
+    for (int i = 1; i < n; ++i) {
+        const int d = ndev > 0 ? (r->device + i) % ndev : r->device;
+        if (wo_dev_create(d, &r->devs[i], err, sizeof err) != 0) {
+            r->devs[i] = NULL;
+            wo_set_error("rank %d on device %d: %s", i, d, err);
+            rc = -1;
+            break;
+        }
+        r->ndevs = (uint32_t)i + 1u;
+        if (wo_dev_enable_peer(r->devs[i], r->dev, err, sizeof err) != 0) {
+            wo_set_error("rank %d on device %d: %s", i, d, err);
+            rc = -1;
+            break;
+        }
+    }
+    if (rc < 0) {
+        for (uint32_t i = 1; i < r->ndevs; ++i) {
+            wo_dev_destroy(r->devs[i]);
+            r->devs[i] = NULL;
+        }
+        r->ndevs = 1;
+    }
+    if (cur >= 0) (void)wo_dev_select(cur);
+    return rc;
+}
+
+int wo_renderer_device_count(Wo_Renderer* r) { return r && r->dev ? (int)r->ndevs : 0; }
 
 void wo_renderer_del(Wo_Renderer* r) {
     if (!r) return;
     (void)wo_renderer_finish(r);
+    for (uint32_t i = 1; i < r->ndevs; ++i) wo_dev_destroy(r->devs[i]);
     if (r->dev) wo_dev_destroy(r->dev);
     free(r->nodes);
     free(r->nonroot);
@@ -370,9 +438,13 @@ static int sync_device(Wo_Renderer* r) {
          * and kernel module are replaced.  wo_dev_upload_scene then drains every
          * other stream of the device (render_rows_device on a caller's stream). */
         if (wo_renderer_finish(r)) return -1;
-        if (wo_dev_upload_scene(r->dev, r->prog, r->n_recs, r->n_prims, r->mats, r->n_mats, err, sizeof err)) {
-            wo_set_error("scene upload failed: %s", err);
-            return -1;
+        const int cur = r->ndevs > 1 ? wo_dev_current() : -1;
+        for (uint32_t i = 0; i < r->ndevs; ++i) {
+            if (wo_dev_upload_scene(r->devs[i], r->prog, r->n_recs, r->n_prims, r->mats, r->n_mats, err,
+                                    sizeof err)) {
+                wo_set_error("scene upload failed (rank %u): %s", i, err);
+                return -1;
+            }
         }
         r->dev_stale = 0;
         r->jit_loaded = 0;
@@ -388,20 +460,29 @@ static int sync_device(Wo_Renderer* r) {
         int want_lanes = lanes_ok && (r->tracer == WO_TRACER_LANES ||
                                       (r->tracer == WO_TRACER_AUTO && r->n_prims > lanes_min));
         int want_jit = !want_lanes && r->tracer != WO_TRACER_INTERPRETER && r->n_prims > 0 && r->n_prims <= max_prims;
-        wo_dev_set_lanes(r->dev, want_lanes);
+        for (uint32_t i = 0; i < r->ndevs; ++i) wo_dev_set_lanes(r->devs[i], want_lanes);
         r->lanes_loaded = want_lanes;
         if (want_jit) {
             char* src = wo_generate_jit_source(r->prog, r->n_recs, r->n_prims);
             if (!src) {
                 fprintf(stderr, WO_LOG_PREFIX " scene specialisation: source generation failed; using the interpreter\n");
-            } else if (wo_dev_set_jit(r->dev, src, err, sizeof err) != 0) {
-                fprintf(stderr, WO_LOG_PREFIX " scene specialisation failed (%s); using the interpreter kernel\n", err);
             } else {
-                r->jit_loaded = 1;
+                /* compiled once (code-object cache), loaded on every rank's device */
+                int ok = 1;
+                for (uint32_t i = 0; i < r->ndevs && ok; ++i) {
+                    if (wo_dev_set_jit(r->devs[i], src, err, sizeof err) != 0) {
+                        fprintf(stderr, WO_LOG_PREFIX " scene specialisation failed (%s); using the interpreter kernel\n",
+                                err);
+                        ok = 0;
+                    }
+                }
+                r->jit_loaded = ok;
             }
             free(src);
         }
-        if (!r->jit_loaded) (void)wo_dev_set_jit(r->dev, NULL, err, sizeof err);
+        if (!r->jit_loaded)
+            for (uint32_t i = 0; i < r->ndevs; ++i) (void)wo_dev_set_jit(r->devs[i], NULL, err, sizeof err);
+        if (cur >= 0) (void)wo_dev_select(cur);
     }
     return 0;
 }
@@ -429,7 +510,10 @@ char const* wo_renderer_trace_path(Wo_Renderer* r) {
     return r->jit_loaded ? "jit" : r->lanes_loaded ? "lanes" : "interpreter";
 }
 
+static int render_sync(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba, int accumulate, int reset);
+
 int wo_renderer_render_f32(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba) {
+    if (r && r->ndevs > 1) return render_sync(r, params, out_rgba, 0, 0) < 0 ? -1 : 0;
     if (sync_device(r)) return -1;
     WoFrame fr;
     if (wo_renderer_frame_desc(r, params, 16, 0, 1, &fr)) return -1;
@@ -516,7 +600,8 @@ static int acc_continues(Wo_Renderer* r, Wo_RenderParams const* p) {
 
 static int submit_frame(Wo_Renderer* r, Wo_RenderParams p, int slot, int accumulate, int reset) {
     char err[256] = {0};
-    long long* d_acc = NULL;
+    long long* d_acc[WO_MAX_DEVICES] = {NULL};
+    int acc = 0;
     uint32_t total = 0;
     if (accumulate && p.mode == WO_SHADING_PATHTRACE) {
         int cont = !reset && acc_continues(r, &p);
@@ -526,10 +611,13 @@ static int submit_frame(Wo_Renderer* r, Wo_RenderParams p, int slot, int accumul
             r->acc_spp = 0;
             r->acc_valid = 1;
         }
-        if (wo_dev_accum_prepare(r->dev, p.width, p.height, !cont, &d_acc, err, sizeof err)) {
-            wo_set_error("accumulation buffer: %s", err);
-            return -1;
+        for (uint32_t i = 0; i < r->ndevs; ++i) {
+            if (wo_dev_accum_prepare(r->devs[i], p.width, p.height, 4, r->ndevs, !cont, &d_acc[i], err, sizeof err)) {
+                wo_set_error("accumulation buffer (rank %u): %s", i, err);
+                return -1;
+            }
         }
+        acc = 1;
         uint64_t t = (uint64_t)r->acc_spp + p.spp;
         if (t > 0xFFFFFFFFull) {
             wo_set_error("accumulated samples overflow");
@@ -540,8 +628,11 @@ static int submit_frame(Wo_Renderer* r, Wo_RenderParams p, int slot, int accumul
         r->acc_spp = total;
     }
     WoFrame fr;
-    if (wo_renderer_frame_desc(r, &p, 4, 0, 1, &fr)) return -1;
-    if (wo_dev_frame_submit(r->dev, &fr, slot, d_acc, total, err, sizeof err)) {
+    if (wo_renderer_frame_desc(r, &p, 4, 0, r->ndevs, &fr)) return -1;
+    const int cur = r->ndevs > 1 ? wo_dev_current() : -1;
+    int rc = wo_dev_frame_submit_ranks(r->devs, r->ndevs, &fr, slot, acc ? d_acc : NULL, total, err, sizeof err);
+    if (cur >= 0) (void)wo_dev_select(cur);
+    if (rc) {
         wo_set_error("frame submit failed: %s", err);
         return -1;
     }
@@ -604,9 +695,14 @@ int wo_renderer_render_accumulate(Wo_Renderer* r, Wo_RenderParams const* params,
         wo_set_error("render_accumulate needs WO_SHADING_PATHTRACE");
         return -1;
     }
+    return render_sync(r, params, out_rgba, 1, reset);
+}
+
+/* One frame through the pipeline's slot 0, waited for (every rank). */
+static int render_sync(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba, int accumulate, int reset) {
     if (wo_renderer_finish(r)) return -1; /* the pipeline's frames first */
     if (sync_device(r)) return -1;
-    if (submit_frame(r, *params, 0, 1, reset)) return -1;
+    if (submit_frame(r, *params, 0, accumulate, reset)) return -1;
     r->pending[0] = 0;
     char err[256] = {0};
     float const* px = NULL;
@@ -615,5 +711,5 @@ int wo_renderer_render_accumulate(Wo_Renderer* r, Wo_RenderParams const* params,
         return -1;
     }
     if (out_rgba) memcpy(out_rgba, px, (size_t)params->width * params->height * 4u * sizeof(float));
-    return (int)r->acc_spp;
+    return accumulate ? (int)r->acc_spp : 0;
 }

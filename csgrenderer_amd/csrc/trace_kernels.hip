@@ -598,6 +598,16 @@ struct WoDev {
     uint32_t* h_bgra[2];
     size_t hbgra_cap[2];
     hipEvent_t slot_ev[2];
+    // several devices per renderer (wo_dev_frame_submit_ranks): on the root,
+    // the rank-major buffer the ranks' shares are copied into and the event that
+    // opens a slot to the ranks; on every other rank, its share of the frame and
+    // the event that marks the share copied
+    float4* d_gather[2];
+    size_t dgather_cap[2];
+    hipEvent_t gate_ev[2];
+    float4* d_part[2];
+    size_t dpart_cap[2];
+    hipEvent_t part_ev[2];
     bool union_only;
     bool lanes_on;
     // scene-specialised kernel (hiprtc)
@@ -616,6 +626,10 @@ extern "C" int wo_dev_count(void) {
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
 }
+
+extern "C" int wo_dev_device(WoDev* dev) { return dev ? dev->device : -1; }
+
+extern "C" int wo_dev_select(int device) { return hipSetDevice(device) == hipSuccess ? 0 : -1; }
 
 extern "C" int wo_dev_current(void) {
     int d = -1;
@@ -670,6 +684,10 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
         if (dev->slot_ev[i]) (void)hipEventDestroy(dev->slot_ev[i]);
         if (dev->d_bgra[i]) (void)hipFree(dev->d_bgra[i]);
         if (dev->h_bgra[i]) (void)hipHostFree(dev->h_bgra[i]);
+        if (dev->d_gather[i]) (void)hipFree(dev->d_gather[i]);
+        if (dev->gate_ev[i]) (void)hipEventDestroy(dev->gate_ev[i]);
+        if (dev->d_part[i]) (void)hipFree(dev->d_part[i]);
+        if (dev->part_ev[i]) (void)hipEventDestroy(dev->part_ev[i]);
     }
     if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
     (void)hipStreamDestroy(dev->stream);
@@ -1198,14 +1216,14 @@ static WoFrame whole_frame(WoFrame const* f) {
     return fr;
 }
 
-extern "C" int wo_dev_accum_prepare(WoDev* dev, uint32_t width, uint32_t height, int reset, long long** d_accum,
-                                    char* err, size_t errlen) {
+extern "C" int wo_dev_accum_prepare(WoDev* dev, uint32_t width, uint32_t height, uint32_t tile_rows,
+                                    uint32_t nranks, int reset, long long** d_accum, char* err, size_t errlen) {
     hipError_t e = hipSetDevice(dev->device);
     if (e != hipSuccess) {
         set_err(err, errlen, "hipSetDevice", e);
         return -1;
     }
-    const size_t bytes = (size_t)width * wo_rank_local_rows(height, 4u, 1u) * 3u * sizeof(long long);
+    const size_t bytes = (size_t)width * wo_rank_local_rows(height, tile_rows, nranks) * 3u * sizeof(long long);
     const long long* old = dev->d_accum;
     if (ensure_buffer(&dev->d_accum, &dev->accum_cap, bytes, err, errlen)) return -1;
     if (reset || dev->d_accum != old) {
@@ -1219,60 +1237,56 @@ extern "C" int wo_dev_accum_prepare(WoDev* dev, uint32_t width, uint32_t height,
     return 0;
 }
 
-extern "C" int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, long long* d_accum,
-                                   uint32_t accum_spp, char* err, size_t errlen) {
-    if (slot < 0 || slot > 1) {
-        snprintf(err, errlen, "bad frame slot %d", slot);
-        return -1;
-    }
-    WoFrame fr = whole_frame(frame);
-    hipError_t e = hipSetDevice(dev->device);
+static int ensure_event(hipEvent_t* ev, char* err, size_t errlen) {
+    if (*ev) return 0;
+    hipError_t e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
-        set_err(err, errlen, "hipSetDevice", e);
+        *ev = nullptr;
+        set_err(err, errlen, "hipEventCreate", e);
         return -1;
     }
-    const size_t pixels = (size_t)fr.width * fr.height;
-    const size_t dbytes = (size_t)fr.width * wo_rank_local_rows(fr.height, fr.tile_rows, 1u) * sizeof(float4);
-    if (ensure_buffer(&dev->d_slot[slot], &dev->dslot_cap[slot], dbytes, err, errlen)) return -1;
-    if (pixels * sizeof(float4) > dev->hslot_cap[slot] || !dev->h_slot[slot]) {
-        if (dev->h_slot[slot]) (void)hipHostFree(dev->h_slot[slot]);
-        dev->h_slot[slot] = nullptr;
-        dev->hslot_cap[slot] = 0;
-        e = hipHostMalloc((void**)&dev->h_slot[slot], pixels ? pixels * sizeof(float4) : 64, hipHostMallocDefault);
-        if (e != hipSuccess) {
-            dev->h_slot[slot] = nullptr;
-            set_err(err, errlen, "hipHostMalloc(frame slot)", e);
-            return -1;
-        }
-        dev->hslot_cap[slot] = pixels * sizeof(float4);
+    return 0;
+}
+
+static int ensure_pinned(void** p, size_t* cap, size_t bytes, char* err, size_t errlen) {
+    if (bytes <= *cap && *p) return 0;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    hipError_t e = hipHostMalloc(p, bytes ? bytes : 64, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        set_err(err, errlen, "hipHostMalloc(frame slot)", e);
+        return -1;
     }
-    if (!dev->slot_ev[slot]) {
-        e = hipEventCreateWithFlags(&dev->slot_ev[slot], hipEventDisableTiming);
-        if (e != hipSuccess) {
-            dev->slot_ev[slot] = nullptr;
-            set_err(err, errlen, "hipEventCreate", e);
-            return -1;
-        }
-    }
-    if (pixels * sizeof(uint32_t) > dev->hbgra_cap[slot] || !dev->h_bgra[slot]) {
-        if (dev->h_bgra[slot]) (void)hipHostFree(dev->h_bgra[slot]);
-        dev->h_bgra[slot] = nullptr;
-        dev->hbgra_cap[slot] = 0;
-        e = hipHostMalloc((void**)&dev->h_bgra[slot], pixels ? pixels * sizeof(uint32_t) : 64, hipHostMallocDefault);
-        if (e != hipSuccess) {
-            dev->h_bgra[slot] = nullptr;
-            set_err(err, errlen, "hipHostMalloc(present slot)", e);
-            return -1;
-        }
-        dev->hbgra_cap[slot] = pixels * sizeof(uint32_t);
-    }
+    *cap = bytes;
+    return 0;
+}
+
+// The slot's buffers on the device that presents (current device = dev's):
+// the device frame (`frame_rows` rows), its pinned host copy, the present
+// encode on both sides and the slot event.
+static int prep_slot(WoDev* dev, int slot, uint32_t width, uint32_t height, uint32_t frame_rows, char* err,
+                     size_t errlen) {
+    const size_t pixels = (size_t)width * height;
+    if (ensure_buffer(&dev->d_slot[slot], &dev->dslot_cap[slot], (size_t)width * frame_rows * sizeof(float4), err,
+                      errlen))
+        return -1;
+    if (ensure_pinned((void**)&dev->h_slot[slot], &dev->hslot_cap[slot], pixels * sizeof(float4), err, errlen))
+        return -1;
+    if (ensure_pinned((void**)&dev->h_bgra[slot], &dev->hbgra_cap[slot], pixels * sizeof(uint32_t), err, errlen))
+        return -1;
     if (ensure_buffer(&dev->d_bgra[slot], &dev->dbgra_cap[slot], pixels * sizeof(uint32_t), err, errlen)) return -1;
-    if (wo_dev_launch_ex(dev, &fr, dev->d_slot[slot], dev->stream, nullptr, d_accum, accum_spp, err, errlen))
-        return -1;
+    return ensure_event(&dev->slot_ev[slot], err, errlen);
+}
+
+// After the frame is in d_slot: the present encode, both copies to the pinned
+// host buffers and the slot event, asynchronous on the device stream.
+static int present_slot(WoDev* dev, int slot, size_t pixels, char* err, size_t errlen) {
+    hipError_t e;
     if (pixels) {
         // the float frame (wo_renderer_last_frame) and its present encode
-        // (wo_renderer_last_frame_bgra8): whole frame, one rank, so the local
-        // rows are the frame rows
+        // (wo_renderer_last_frame_bgra8)
         if (wo_dev_srgb8(dev->d_slot[slot], dev->d_bgra[slot], pixels, dev->stream, err, errlen)) return -1;
         e = hipMemcpyAsync(dev->h_slot[slot], dev->d_slot[slot], pixels * sizeof(float4), hipMemcpyDeviceToHost,
                            dev->stream);
@@ -1290,6 +1304,118 @@ extern "C" int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, l
         return -1;
     }
     return 0;
+}
+
+extern "C" int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, long long* d_accum,
+                                   uint32_t accum_spp, char* err, size_t errlen) {
+    if (slot < 0 || slot > 1) {
+        snprintf(err, errlen, "bad frame slot %d", slot);
+        return -1;
+    }
+    WoFrame fr = whole_frame(frame);
+    hipError_t e = hipSetDevice(dev->device);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipSetDevice", e);
+        return -1;
+    }
+    if (prep_slot(dev, slot, fr.width, fr.height, wo_rank_local_rows(fr.height, fr.tile_rows, 1u), err, errlen))
+        return -1;
+    if (wo_dev_launch_ex(dev, &fr, dev->d_slot[slot], dev->stream, nullptr, d_accum, accum_spp, err, errlen))
+        return -1;
+    // whole frame, one rank: the local rows are the frame rows
+    return present_slot(dev, slot, (size_t)fr.width * fr.height, err, errlen);
+}
+
+extern "C" int wo_dev_enable_peer(WoDev* from, WoDev* to, char* err, size_t errlen) {
+    if (from->device == to->device) return 0;
+    int can = 0;
+    hipError_t e = hipDeviceCanAccessPeer(&can, from->device, to->device);
+    if (e != hipSuccess || !can) return 0;  // the copies then go through the runtime's staging path
+    e = hipSetDevice(from->device);
+    if (e == hipSuccess) e = hipDeviceEnablePeerAccess(to->device, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) {
+        (void)hipGetLastError();
+        e = hipSuccess;
+    }
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipDeviceEnablePeerAccess", e);
+        return -1;
+    }
+    return 0;
+}
+
+// A frame over n ranks: rank i renders its row-cyclic 4-row
+// tiles on its own device and stream; ranks 1..n-1 copy their share into the
+// root's rank-major gather buffer (peer DMA over xGMI when the devices differ)
+// and the root un-interleaves the gathered shares into the slot's frame, then
+// presents as for one device.  Every step is asynchronous; the streams are
+// ordered by events only (gate: the slot's previous use on the root is done;
+// part_ev: a rank's copy is done).
+extern "C" int wo_dev_frame_submit_ranks(WoDev* const* devs, uint32_t n, WoFrame const* frame, int slot,
+                                         long long* const* d_accum, uint32_t accum_spp, char* err, size_t errlen) {
+    if (n <= 1u) return wo_dev_frame_submit(devs[0], frame, slot, d_accum ? d_accum[0] : nullptr, accum_spp, err, errlen);
+    if (slot < 0 || slot > 1) {
+        snprintf(err, errlen, "bad frame slot %d", slot);
+        return -1;
+    }
+    WoDev* root = devs[0];
+    WoFrame fr = *frame;
+    fr.tile_rows = 4;
+    fr.nranks = n;
+    const uint32_t lr = wo_rank_local_rows(fr.height, fr.tile_rows, n);
+    const size_t share = (size_t)lr * fr.width;  // float4s per rank
+    const size_t pixels = (size_t)fr.width * fr.height;
+    hipError_t e = hipSetDevice(root->device);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipSetDevice", e);
+        return -1;
+    }
+    if (prep_slot(root, slot, fr.width, fr.height, fr.height, err, errlen)) return -1;
+    if (ensure_buffer(&root->d_gather[slot], &root->dgather_cap[slot], share * n * sizeof(float4), err, errlen))
+        return -1;
+    if (ensure_event(&root->gate_ev[slot], err, errlen)) return -1;
+    e = hipEventRecord(root->gate_ev[slot], root->stream);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipEventRecord(gate)", e);
+        return -1;
+    }
+    // rank 0 renders straight into its slice of the gather buffer
+    fr.rank = 0;
+    if (wo_dev_launch_ex(root, &fr, root->d_gather[slot], root->stream, nullptr, d_accum ? d_accum[0] : nullptr,
+                         accum_spp, err, errlen))
+        return -1;
+    for (uint32_t i = 1; i < n; ++i) {
+        WoDev* dv = devs[i];
+        fr.rank = i;
+        e = hipSetDevice(dv->device);
+        if (e != hipSuccess) {
+            set_err(err, errlen, "hipSetDevice", e);
+            return -1;
+        }
+        if (ensure_buffer(&dv->d_part[slot], &dv->dpart_cap[slot], share * sizeof(float4), err, errlen)) return -1;
+        if (ensure_event(&dv->part_ev[slot], err, errlen)) return -1;
+        e = hipStreamWaitEvent(dv->stream, root->gate_ev[slot], 0);
+        if (e != hipSuccess) {
+            set_err(err, errlen, "hipStreamWaitEvent(gate)", e);
+            return -1;
+        }
+        if (wo_dev_launch_ex(dv, &fr, dv->d_part[slot], dv->stream, nullptr, d_accum ? d_accum[i] : nullptr,
+                             accum_spp, err, errlen))
+            return -1;
+        e = hipMemcpyPeerAsync(root->d_gather[slot] + share * i, root->device, dv->d_part[slot], dv->device,
+                               share * sizeof(float4), dv->stream);
+        if (e == hipSuccess) e = hipEventRecord(dv->part_ev[slot], dv->stream);
+        if (e == hipSuccess) e = hipSetDevice(root->device);
+        if (e == hipSuccess) e = hipStreamWaitEvent(root->stream, dv->part_ev[slot], 0);
+        if (e != hipSuccess) {
+            set_err(err, errlen, "gather copy", e);
+            return -1;
+        }
+    }
+    if (wo_dev_assemble(root->d_gather[slot], root->d_slot[slot], fr.width, fr.height, fr.tile_rows, n,
+                        root->stream, err, errlen))
+        return -1;
+    return present_slot(root, slot, pixels, err, errlen);
 }
 
 extern "C" int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, uint32_t const** host_bgra8, char* err,

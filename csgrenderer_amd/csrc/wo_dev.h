@@ -47,16 +47,31 @@ int wo_dev_launch(WoDev* dev, WoFrame const* frame, void* d_out, void* stream,
 int wo_dev_launch_ex(WoDev* dev, WoFrame const* frame, void* d_out, void* stream,
                      unsigned long long* d_segments, long long* d_accum, uint32_t accum_spp, char* err,
                      size_t errlen);
-/* Progressive accumulation buffer for a width x height frame (3 int64 per
- * pixel), zeroed (async, on the device stream) when `reset` or reallocated. */
-int wo_dev_accum_prepare(WoDev* dev, uint32_t width, uint32_t height, int reset, long long** d_accum, char* err,
-                         size_t errlen);
+/* Progressive accumulation buffer for one rank's share of a width x height
+ * frame (row-cyclic tiles of tile_rows rows over nranks; 3 int64 per pixel),
+ * zeroed (async, on the device stream) when `reset` or reallocated. */
+int wo_dev_accum_prepare(WoDev* dev, uint32_t width, uint32_t height, uint32_t tile_rows, uint32_t nranks, int reset,
+                         long long** d_accum, char* err, size_t errlen);
 /* The draw_frame pipeline: render a whole frame into frame slot 0 or 1 (with
  * accumulation when d_accum), encode it for present (sRGB, B8G8R8A8), copy both
  * to the slot's pinned host buffers and record the slot's event -- all
  * asynchronous on the device stream. */
 int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, long long* d_accum, uint32_t accum_spp,
                         char* err, size_t errlen);
+/* wo_dev_frame_submit over n ranks, devs[0] presenting: rank i renders its
+ * row-cyclic 4-row tiles on devs[i] (d_accum[i]: its accumulation, or d_accum
+ * NULL), ranks 1..n-1 copy their shares to devs[0] (peer DMA when the devices
+ * differ), devs[0] assembles the frame into the slot.  Asynchronous; wait with
+ * wo_dev_frame_wait(devs[0], slot, ...). */
+int wo_dev_frame_submit_ranks(WoDev* const* devs, uint32_t n, WoFrame const* frame, int slot,
+                              long long* const* d_accum, uint32_t accum_spp, char* err, size_t errlen);
+/* Let `from`'s device access `to`'s memory directly (no-op on one device, or
+ * when the pair has no peer path). */
+int wo_dev_enable_peer(WoDev* from, WoDev* to, char* err, size_t errlen);
+/* HIP device of a WoDev. */
+int wo_dev_device(WoDev* dev);
+/* Select a HIP device for the calling thread (restoring the caller's). */
+int wo_dev_select(int device);
 /* Wait for the slot's frame; *host = its pixels (RGBA float), *host_bgra8 (if
  * non-NULL) = its present encode; both valid until the slot is submitted again. */
 int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, uint32_t const** host_bgra8, char* err,

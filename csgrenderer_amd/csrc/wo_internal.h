@@ -18,6 +18,8 @@
 #include "wololo/wo_scene.h"
 #include "wo_dev.h"
 
+#define WO_MAX_DEVICES 16
+
 /* Node kinds: same order as the reference's NodeType (renderer.c:182-188). */
 enum {
     WO_NODE_SPHERE = 0,
@@ -64,7 +66,9 @@ struct Wo_Renderer {
     int dev_stale;      /* device copy out of date */
 
     int device;         /* -1: device-less (tests only) */
-    WoDev* dev;
+    WoDev* dev;         /* rank 0: uploads, presents (== devs[0]) */
+    uint32_t ndevs;     /* ranks a frame is split over (wo_renderer_set_devices) */
+    WoDev* devs[WO_MAX_DEVICES];
 
     int tracer;         /* Wo_Tracer */
     int jit_loaded;     /* the device runs the scene-specialised kernel */

@@ -107,6 +107,8 @@ SIGNATURES = {
     "wo_renderer_render_rows_device": (c_int, [c_void_p, POINTER(RenderParams), c_void_p, c_uint32, c_uint32,
                                                c_uint32, c_void_p, c_void_p]),
     "wo_assemble_rows_device": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_void_p]),
+    "wo_renderer_set_devices": (c_int, [c_void_p, c_int]),
+    "wo_renderer_device_count": (c_int, [c_void_p]),
     "wo_renderer_finish": (c_int, [c_void_p]),
     "wo_renderer_last_frame": (POINTER(c_float), [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
     "wo_renderer_last_frame_bgra8": (POINTER(c_uint32), [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
@@ -319,6 +321,16 @@ class Renderer:
     def draw_frame(self):
         """wo_renderer_draw_frame (pipelined: presents the previous frame)."""
         self.lib.wo_renderer_draw_frame(self.ptr)
+
+    def set_devices(self, n: int) -> int:
+        """Split every frame over n ranks (renderer_ext.h wo_renderer_set_devices)."""
+        rc = self.lib.wo_renderer_set_devices(self.ptr, int(n))
+        if rc < 0:
+            raise WololoError(last_error())
+        return rc
+
+    def device_count(self) -> int:
+        return int(self.lib.wo_renderer_device_count(self.ptr))
 
     def finish(self):
         if self.lib.wo_renderer_finish(self.ptr):

@@ -79,6 +79,22 @@ int wo_renderer_render_rows_device(Wo_Renderer* r, Wo_RenderParams const* params
 int wo_assemble_rows_device(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,
                             uint32_t tile_rows, uint32_t nranks, void* stream);
 
+/* ---- several GPUs per renderer ----
+ * The reference renders on physical device 0 only (renderer.c:519-520).  Here
+ * one renderer can split every frame over n ranks: rank i renders the
+ * row-cyclic 4-row tiles g with g % n == i on HIP device (d0 + i) mod
+ * visible devices (d0 = wo_renderer_device), ranks 1..n-1 copy their share to
+ * d0 (peer DMA over xGMI), and d0 assembles and presents the frame.  The image
+ * is the same bit for bit for every n.  n above the device count stacks ranks
+ * on one device.  draw_frame, render_f32 and render_accumulate use every rank;
+ * render_rows_device (the caller splits the frame) uses d0 only.
+ * Default: WOLOLO_DEVICES=N|all, else all visible GPUs for a renderer created
+ * with an app (the demo) and 1 without.  Returns n, or -1 (last_error; the
+ * renderer then keeps one rank). */
+int wo_renderer_set_devices(Wo_Renderer* r, int n);
+/* Ranks a frame is split over (0 for a device-less renderer). */
+int wo_renderer_device_count(Wo_Renderer* r);
+
 /* ---- frame pipeline and progressive rendering ----
  * The reference's draw_frame_with_renderer (renderer.c:2085-2219) ends every
  * frame with vkQueueWaitIdle (2212).  wo_renderer_draw_frame instead submits

@@ -118,3 +118,70 @@ def test_present_encode_and_ppm_dump(tmp_path, monkeypatch):
     assert np.array_equal(img.astype(np.int64), want)
     r.close()
     assert os.path.getsize(out) > 0
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_multi_rank_renderer_equals_one_device(nranks):
+    """wo_renderer_set_devices (renderer_ext.h): every frame split over n ranks as
+    row-cyclic 4-row tiles, shares copied to rank 0 and assembled there.  On a
+    one-GPU box the ranks stack on one device, each with its own stream and
+    buffers, so the rank streams, the gather copies and the events that order
+    them all run.  The images equal one rank's bit for bit: render_f32, the
+    draw_frame pipeline and progressive accumulation, for the specialised kernel,
+    the lane tracer and the reference shader."""
+    r = wl.Renderer("ranks", max_nodes=4096)
+    info = scenes.build("csg32", r)
+    assert r.device_count() == 1
+    p = info.params(width=203, height=117, spp=3, seed=5)
+    one = r.render(p)
+    shader = wl.render_params(203, 117, time_sec=0.61)
+    one_shader = r.render(shader)
+    acc1, _ = r.render_accumulate(p, reset=True)
+    acc2, n2 = r.render_accumulate(p)
+    assert r.set_devices(nranks) == nranks and r.device_count() == nranks
+    wl.clear_error()
+    _cmp(r.render(p), one, f"csg32 over {nranks} ranks")
+    assert r.trace_path() == "jit"
+    _cmp(r.render(shader), one_shader, f"reference shader over {nranks} ranks")
+    # the pipeline: two frames in flight across the ranks
+    r.set_draw_params(p)
+    r.draw_frame()
+    r.draw_frame()
+    r.finish()
+    _cmp(r.last_frame(), one, f"draw_frame over {nranks} ranks")
+    b = r.last_frame_bgra8()
+    assert np.array_equal(b, wl.srgb8_encode_host(one))
+    # progressive accumulation: per-rank sums, the same mean as on one rank
+    g1, _ = r.render_accumulate(p, reset=True)
+    g2, m2 = r.render_accumulate(p)
+    assert m2 == n2 == 2 * p.spp
+    _cmp(g1, acc1, "accumulation, first frame")
+    _cmp(g2, acc2, "accumulation, second frame")
+    assert wl.last_error() == ""
+    # back to one rank
+    assert r.set_devices(1) == 1
+    _cmp(r.render(p), one, "back to one rank")
+    r.close()
+
+
+def test_multi_rank_lanes_and_scene_change():
+    """Union-only scene on the lane tracer over 4 ranks; then a node is added with a
+    frame in flight: every rank gets the new scene before the next frame."""
+    r = wl.Renderer("ranks-lanes", max_nodes=4096)
+    info = scenes.build("rtiow_cover", r)
+    p = info.params(width=96, height=64, spp=2, seed=1)
+    one = r.render(p)
+    r.set_devices(4)
+    _cmp(r.render(p), one, "rtiow over 4 ranks")
+    assert r.trace_path() == "lanes"
+    r.set_draw_params(p)
+    r.draw_frame()
+    extra = r.sphere(0.7)
+    r.union(wl.arg(extra, (0.0, 1.0, 2.0)), wl.arg(r.sphere(0.2), (1.0, 0.5, 2.5)))
+    r.draw_frame()
+    r.finish()
+    new4 = r.last_frame()
+    r.set_devices(1)
+    _cmp(new4, r.render(p), "new scene over 4 ranks")
+    assert not np.array_equal(new4, one)
+    r.close()
