@@ -505,6 +505,11 @@ char* wo_renderer_jit_source(Wo_Renderer* r) {
 
 void wo_free(void* p) { free(p); }
 
+int wo_renderer_jit_info(Wo_Renderer* r, double* seconds) {
+    if (!r || !r->dev || !r->jit_loaded) return -1;
+    return wo_dev_jit_origin(r->dev, seconds);
+}
+
 char const* wo_renderer_trace_path(Wo_Renderer* r) {
     if (!r->dev) return "none";
     return r->jit_loaded ? "jit" : r->lanes_loaded ? "lanes" : "interpreter";

@@ -613,7 +613,8 @@ struct WoDev {
     // scene-specialised kernel (hiprtc)
     hipModule_t jit_module;
     hipFunction_t jit_fn;
-    uint64_t jit_hash;
+    std::string jit_key;  // SHA-256 (hex) of the loaded code object's inputs
+    int jit_origin;       // 0 process cache, 1 disk cache, 2 compiled
     double jit_compile_sec;
 };
 
@@ -832,15 +833,11 @@ extern "C" int wo_dev_upload_scene(WoDev* dev, WoRec const* prog, uint32_t n_rec
 
 // ---- scene-specialised kernels (hiprtc) ----
 
-static uint64_t fnv1a(const char* s, size_t n, uint64_t h = 1469598103934665603ull) {
-    for (size_t i = 0; i < n; ++i) h = (h ^ (unsigned char)s[i]) * 1099511628211ull;
-    return h;
-}
-
-// Process-wide cache of compiled code objects (the same scene compiled once).
+// Process-wide cache of compiled code objects (the same scene compiled once per
+// process), in front of the on-disk cache (jit_cache.c) shared by processes.
 static std::mutex g_jit_mu;
-static std::unordered_map<uint64_t, std::vector<char>>& jit_cache() {
-    static std::unordered_map<uint64_t, std::vector<char>> m;
+static std::unordered_map<std::string, std::vector<char>>& jit_cache() {
+    static std::unordered_map<std::string, std::vector<char>> m;
     return m;
 }
 
@@ -863,6 +860,12 @@ static std::vector<std::string> jit_extra_flags() {
     return out;
 }
 
+static std::vector<std::string> jit_options(const std::string& arch) {
+    std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-ffp-contract=off", "-std=c++17"};
+    for (const std::string& f : jit_extra_flags()) opts.push_back(f);
+    return opts;
+}
+
 static int jit_compile(const char* src, const std::string& arch, std::vector<char>& code, char* err, size_t errlen) {
     hiprtcProgram p;
     const char* hdr_src[] = {kEmbed_wo_device_common_h, kEmbed_wo_scene_h};
@@ -871,10 +874,9 @@ static int jit_compile(const char* src, const std::string& arch, std::vector<cha
         snprintf(err, errlen, "hiprtcCreateProgram failed");
         return -1;
     }
-    std::string arch_opt = "--offload-arch=" + arch;
-    std::vector<std::string> extra = jit_extra_flags();
-    std::vector<const char*> opts = {arch_opt.c_str(), "-O3", "-ffp-contract=off", "-std=c++17"};
-    for (const std::string& f : extra) opts.push_back(f.c_str());
+    std::vector<std::string> opt_s = jit_options(arch);
+    std::vector<const char*> opts;
+    for (const std::string& o : opt_s) opts.push_back(o.c_str());
     hiprtcResult rc = hiprtcCompileProgram(p, (int)opts.size(), opts.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t ls = 0;
@@ -893,6 +895,78 @@ static int jit_compile(const char* src, const std::string& arch, std::vector<cha
     return 0;
 }
 
+// SHA-256 over everything the code object depends on: a format tag, the hiprtc
+// version, the target, the options (WOLOLO_JIT_FLAGS included), the embedded
+// headers and the generated source; each part length-prefixed.
+static std::string jit_key(const char* src, const std::string& arch) {
+    WoSha256 s;
+    wo_sha256_init(&s);
+    auto part = [&](const char* p, size_t n) {
+        const uint64_t len = n;
+        wo_sha256_update(&s, &len, sizeof len);
+        wo_sha256_update(&s, p, n);
+    };
+    part("wololo-jit-1", 12);
+    int vmaj = 0, vmin = 0;
+    (void)hiprtcVersion(&vmaj, &vmin);
+    const int ver[2] = {vmaj, vmin};
+    part((const char*)ver, sizeof ver);
+    part(arch.data(), arch.size());
+    for (const std::string& o : jit_options(arch)) part(o.data(), o.size());
+    part(kEmbed_wo_device_common_h, strlen(kEmbed_wo_device_common_h));
+    part(kEmbed_wo_scene_h, strlen(kEmbed_wo_scene_h));
+    part(src, strlen(src));
+    uint8_t dg[32];
+    wo_sha256_final(&s, dg);
+    char hex[65];
+    wo_sha256_hex(dg, hex);
+    return std::string(hex);
+}
+
+static int jit_code(const char* src, const std::string& arch, std::vector<char>& code, std::string& key, int& origin,
+                    double& seconds, char* err, size_t errlen) {
+    auto t0 = std::chrono::steady_clock::now();
+    key = jit_key(src, arch);
+    {
+        std::lock_guard<std::mutex> lock(g_jit_mu);
+        auto it = jit_cache().find(key);
+        if (it != jit_cache().end()) {
+            code = it->second;
+            origin = 0;
+        }
+    }
+    if (code.empty()) {
+        void* buf = nullptr;
+        size_t n = 0;
+        if (wo_jit_disk_load(key.c_str(), &buf, &n) == 0) {
+            code.assign((char*)buf, (char*)buf + n);
+            free(buf);
+            origin = 1;
+        } else {
+            if (jit_compile(src, arch, code, err, errlen)) return -1;
+            origin = 2;
+            (void)wo_jit_disk_store(key.c_str(), code.data(), code.size());  // best effort
+        }
+        std::lock_guard<std::mutex> lock(g_jit_mu);
+        jit_cache()[key] = code;
+    }
+    seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+extern "C" long long wo_jit_code_object(const char* src, const char* arch, int* origin, double* seconds,
+                                        char* key_hex, char* err, size_t errlen) {
+    std::vector<char> code;
+    std::string key;
+    int org = -1;
+    double sec = 0.0;
+    if (jit_code(src, arch ? std::string(arch) : std::string("gfx950"), code, key, org, sec, err, errlen)) return -1;
+    if (origin) *origin = org;
+    if (seconds) *seconds = sec;
+    if (key_hex) snprintf(key_hex, 65, "%s", key.c_str());
+    return (long long)code.size();
+}
+
 extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t errlen) {
     hipError_t e = hipSetDevice(dev->device);
     if (e != hipSuccess) {
@@ -903,26 +977,16 @@ extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t err
         if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
         dev->jit_module = nullptr;
         dev->jit_fn = nullptr;
-        dev->jit_hash = 0;
+        dev->jit_key.clear();
+        dev->jit_origin = -1;
         return 0;
     }
-    const char* flags = getenv("WOLOLO_JIT_FLAGS");
-    uint64_t h = fnv1a(dev->arch.data(), dev->arch.size(), fnv1a(src, strlen(src)));
-    if (flags) h = fnv1a(flags, strlen(flags), h);
-    if (dev->jit_fn && dev->jit_hash == h) return 0;
     std::vector<char> code;
-    {
-        std::lock_guard<std::mutex> lock(g_jit_mu);
-        auto it = jit_cache().find(h);
-        if (it != jit_cache().end()) code = it->second;
-    }
-    if (code.empty()) {
-        auto t0 = std::chrono::steady_clock::now();
-        if (jit_compile(src, dev->arch, code, err, errlen)) return -1;
-        dev->jit_compile_sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        std::lock_guard<std::mutex> lock(g_jit_mu);
-        jit_cache()[h] = code;
-    }
+    std::string key;
+    int origin = -1;
+    double sec = 0.0;
+    if (dev->jit_fn && dev->jit_key == jit_key(src, dev->arch)) return 0;
+    if (jit_code(src, dev->arch, code, key, origin, sec, err, errlen)) return -1;
     hipModule_t mod = nullptr;
     e = hipModuleLoadData(&mod, code.data());
     if (e != hipSuccess) {
@@ -939,8 +1003,16 @@ extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t err
     if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
     dev->jit_module = mod;
     dev->jit_fn = fn;
-    dev->jit_hash = h;
+    dev->jit_key = key;
+    dev->jit_origin = origin;
+    dev->jit_compile_sec = sec;
     return 0;
+}
+
+extern "C" int wo_dev_jit_origin(WoDev* dev, double* seconds) {
+    if (!dev || !dev->jit_fn) return -1;
+    if (seconds) *seconds = dev->jit_compile_sec;
+    return dev->jit_origin;
 }
 
 extern "C" int wo_jit_compile_check(const char* src, const char* arch, char* err, size_t errlen) {

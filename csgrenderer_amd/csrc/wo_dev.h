@@ -72,6 +72,26 @@ int wo_dev_enable_peer(WoDev* from, WoDev* to, char* err, size_t errlen);
 int wo_dev_device(WoDev* dev);
 /* Select a HIP device for the calling thread (restoring the caller's). */
 int wo_dev_select(int device);
+/* jit_cache.c: SHA-256 and the on-disk code-object cache of the specialised
+ * kernels (keyed by the hex digest of everything that determines the object). */
+typedef struct WoSha256 {
+    uint32_t h[8];
+    uint64_t len;
+    uint8_t buf[64];
+    uint32_t fill;
+} WoSha256;
+void wo_sha256_init(WoSha256* s);
+void wo_sha256_update(WoSha256* s, const void* data, size_t n);
+void wo_sha256_final(WoSha256* s, uint8_t out[32]);
+void wo_sha256_hex(const uint8_t digest[32], char out[65]);
+int wo_jit_cache_dir(char* out, size_t len);
+/* 0 and a malloc'd copy of the object on a valid entry, else -1 */
+int wo_jit_disk_load(const char* key_hex, void** code, size_t* size);
+int wo_jit_disk_store(const char* key_hex, const void* code, size_t size);
+/* wo_jit_code_object: renderer_ext.h */
+/* Origin (as above; -1: no specialised kernel) and seconds of the object the
+ * device's specialised kernel was loaded from. */
+int wo_dev_jit_origin(WoDev* dev, double* seconds);
 /* Wait for the slot's frame; *host = its pixels (RGBA float), *host_bgra8 (if
  * non-NULL) = its present encode; both valid until the slot is submitted again. */
 int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, uint32_t const** host_bgra8, char* err,

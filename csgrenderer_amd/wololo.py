@@ -128,6 +128,9 @@ SIGNATURES = {
     "wo_renderer_trace_path": (c_char_p, [c_void_p]),
     "wo_renderer_jit_source": (c_void_p, [c_void_p]),
     "wo_jit_compile_check": (c_int, [c_char_p, c_char_p, c_char_p, c_size_t]),
+    "wo_jit_code_object": (ctypes.c_longlong, [c_char_p, c_char_p, POINTER(c_int), POINTER(c_double), c_char_p,
+                                               c_char_p, c_size_t]),
+    "wo_renderer_jit_info": (c_int, [c_void_p, POINTER(c_double)]),
     "wo_free": (None, [c_void_p]),
     "wo_renderer_node_count": (c_size_t, [c_void_p]),
     "wo_renderer_name": (c_char_p, [c_void_p]),
@@ -281,6 +284,12 @@ class Renderer:
         finally:
             self.lib.wo_free(p)
 
+    def jit_info(self):
+        """(origin, seconds) of the specialised kernel: origin "process" / "disk" / "compiled", or None."""
+        sec = c_double(0.0)
+        o = self.lib.wo_renderer_jit_info(self.ptr, ctypes.byref(sec))
+        return (None if o < 0 else JIT_ORIGINS[o]), sec.value
+
     def set_jit(self, mode: int):
         self.lib.wo_renderer_set_jit(self.ptr, int(mode))
 
@@ -410,6 +419,21 @@ def abi_layout(type_name: str, field: str | None = None) -> int:
     """sizeof / offsetof as the C library was compiled (wo_abi_layout); -1 if unknown."""
     v = load().wo_abi_layout(type_name.encode(), field.encode() if field else None)
     return -1 if v == ctypes.c_size_t(-1).value else int(v)
+
+
+JIT_ORIGINS = ("process", "disk", "compiled")
+
+
+def jit_code_object(src: str, arch: str = "gfx950"):
+    """(size, origin, seconds, key) of the specialised kernel's code object (wo_jit_code_object)."""
+    err = ctypes.create_string_buffer(4096)
+    key = ctypes.create_string_buffer(65)
+    org, sec = c_int(-1), c_double(0.0)
+    n = load().wo_jit_code_object(src.encode(), arch.encode(), ctypes.byref(org), ctypes.byref(sec), key, err,
+                                  len(err))
+    if n < 0:
+        raise WololoError(err.value.decode(errors="replace"))
+    return int(n), JIT_ORIGINS[org.value], sec.value, key.value.decode()
 
 
 def jit_compile_check(src: str, arch: str = "gfx950") -> str:

@@ -176,6 +176,19 @@ char* wo_renderer_jit_source(Wo_Renderer* r);
 /* Compile `src` with hiprtc for `arch` (e.g. "gfx950") without loading it --
  * needs no GPU.  Returns 0, or -1 with the compiler log in err. */
 int wo_jit_compile_check(char const* src, char const* arch, char* err, size_t errlen);
+/* Code object of the specialised kernel `src` for `arch`, as a render would get
+ * it: from this process's cache, else the on-disk cache (WOLOLO_JIT_CACHE =
+ * directory, "0" = off; default $XDG_CACHE_HOME/wololo/jit or
+ * ~/.cache/wololo/jit; entries keyed by the SHA-256 of source, headers,
+ * target, options and hiprtc version), else compiled with hiprtc and stored.
+ * *origin: 0 process cache, 1 disk cache, 2 compiled; *seconds: time taken;
+ * key_hex (65 bytes or NULL): the key.  Returns the object's size or -1 (err).
+ * Needs no GPU. */
+long long wo_jit_code_object(char const* src, char const* arch, int* origin, double* seconds, char* key_hex,
+                             char* err, size_t errlen);
+/* Where the renderer's specialised kernel came from (origin as above; -1: the
+ * renderer does not run one) and the seconds it took (compile or load). */
+int wo_renderer_jit_info(Wo_Renderer* r, double* seconds);
 void wo_free(void* p);
 
 size_t wo_renderer_node_count(Wo_Renderer* r);

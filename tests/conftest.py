@@ -7,6 +7,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
+# the specialised kernels' on-disk code-object cache stays inside the tree
+os.environ.setdefault("WOLOLO_JIT_CACHE", os.path.join(ROOT, ".jit_cache"))
 
 
 def pytest_configure(config):

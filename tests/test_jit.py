@@ -86,3 +86,112 @@ def test_member_skip_guards(hostonly, monkeypatch):
     monkeypatch.setenv("WOLOLO_JIT_MEMBER_SKIP", "0")
     assert guard not in r.jit_source()
     r.close()
+
+
+_CHILD = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+from csgrenderer_amd import wololo as wl
+src = open({src!r}).read()
+n, origin, sec, key = wl.jit_code_object(src, "gfx950")
+print(json.dumps({{"n": n, "origin": origin, "sec": sec, "key": key}}))
+"""
+
+
+def _child(tmp_path, src_text, env_extra=None):
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sp = tmp_path / f"src{abs(hash(src_text)) % 10**8}.hip"
+    sp.write_text(src_text)
+    env = dict(os.environ, WOLOLO_JIT_CACHE=str(tmp_path / "cache"))
+    env.pop("WOLOLO_JIT_FLAGS", None)
+    env.update(env_extra or {})
+    out = subprocess.run([sys.executable, "-c", _CHILD.format(root=root, src=str(sp))], env=env, check=True,
+                         capture_output=True, text=True, timeout=300).stdout
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def test_persistent_code_object_cache(hostonly, tmp_path, monkeypatch):
+    """The specialised kernel's code object is cached on disk under the SHA-256 of its
+    inputs: a second process loads it instead of compiling; a changed scene or a changed
+    compile flag misses; a corrupt entry is a miss and is rewritten."""
+    import hashlib
+    import struct
+    r = wl.Renderer("cache", max_nodes=64)
+    a = r.sphere(0.5)
+    b = r.sphere(0.3)
+    r.difference(wl.arg(a), wl.arg(b, (0.2, 0.0, 0.0)))
+    src = r.jit_source()
+    r.sphere(0.25)  # another root: another scene
+    src2 = r.jit_source()
+    r.close()
+    assert src != src2
+    first = _child(tmp_path, src)
+    assert first["origin"] == "compiled" and first["n"] > 0
+    entry = tmp_path / "cache" / f"{first['key']}.co"
+    data = entry.read_bytes()
+    assert data[:8] == b"WOJITCO1"
+    (n,) = struct.unpack("<Q", data[8:16])
+    assert n == first["n"] == len(data) - 48
+    assert data[16:48] == hashlib.sha256(data[48:]).digest()  # the library's SHA-256 is FIPS 180-4's
+    second = _child(tmp_path, src)
+    assert second["origin"] == "disk" and second["key"] == first["key"] and second["n"] == first["n"]
+    assert second["sec"] < 0.5
+    other = _child(tmp_path, src2)
+    assert other["origin"] == "compiled" and other["key"] != first["key"]
+    flagged = _child(tmp_path, src, {"WOLOLO_JIT_FLAGS": "-DWO_LDS_NEXT_EAGER=1"})
+    assert flagged["origin"] == "compiled" and flagged["key"] != first["key"]
+    # a truncated / corrupted entry is not loaded
+    entry.write_bytes(data[:-7] + b"garbage")
+    again = _child(tmp_path, src)
+    assert again["origin"] == "compiled" and again["key"] == first["key"]
+    assert entry.read_bytes() == data  # rewritten, same object
+    # off switch
+    off = _child(tmp_path, src, {"WOLOLO_JIT_CACHE": "0"})
+    assert off["origin"] == "compiled"
+    # same process: the process cache
+    monkeypatch.setenv("WOLOLO_JIT_CACHE", str(tmp_path / "cache"))
+    n, origin, _, key = wl.jit_code_object(src, "gfx950")
+    n2, origin2, _, key2 = wl.jit_code_object(src, "gfx950")
+    assert origin2 == "process" and key2 == key == first["key"] and n2 == n
+
+
+_RENDER_CHILD = r"""
+import json, sys, time
+sys.path.insert(0, {root!r})
+from csgrenderer_amd import scenes
+from csgrenderer_amd import wololo as wl
+r = wl.Renderer("cache-child", max_nodes=4096)
+info = scenes.build("csg256_balanced", r)
+t0 = time.perf_counter()
+img = r.render(info.params(width=64, height=36, spp=2))
+origin, sec = r.jit_info()
+print(json.dumps({{"origin": origin, "sec": sec, "wall": time.perf_counter() - t0, "sum": float(img.sum()),
+                   "path": r.trace_path()}}))
+"""
+
+
+@pytest.mark.gpu
+def test_second_process_renders_csg256_without_compiling(tmp_path):
+    """csg256 compiles for seconds; a second process with the same cache loads the code
+    object from disk (< 0.5 s) and renders the same image."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WOLOLO_JIT_CACHE=str(tmp_path / "cache"))
+    env.pop("WOLOLO_JIT_FLAGS", None)
+    runs = []
+    for _ in range(2):
+        out = subprocess.run([sys.executable, "-c", _RENDER_CHILD.format(root=root)], env=env, check=True,
+                             capture_output=True, text=True, timeout=150).stdout
+        runs.append(json.loads(out.strip().splitlines()[-1]))
+    assert runs[0]["path"] == runs[1]["path"] == "jit"
+    assert runs[0]["origin"] == "compiled"
+    assert runs[1]["origin"] == "disk" and runs[1]["sec"] < 0.5, runs
+    assert runs[1]["sum"] == runs[0]["sum"]
+    print(runs)
