@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--tile-rows", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-count-work", action="store_true",
+                    help="skip the executed-work counting frame (roofline.achieved then uses the brute-force count)")
     ap.add_argument("--tracer", default=os.environ.get("WOLOLO_TRACER", "auto"),
                     choices=["auto", "interpreter", "jit", "lanes"],
                     help="path-tracer kernel (renderer_ext.h Wo_Tracer); results are identical")
@@ -173,6 +175,14 @@ def main():
     segs_local = int(seg.item())
     segs_all = int(segs_total.item())
     k_ms = sum(k_start[i].elapsed_time(k_end[i]) for i in range(args.steps)) / args.steps
+    # executed work of this rank's share: one more frame with the counting variant of
+    # the same kernel, outside the timed region (wo_renderer_count_work)
+    work = None
+    if rank == 0 and info.mode == wl.MODE_PATHTRACE and not args.no_count_work:
+        work = r.count_work(params, T, rank, world)
+        if work["segments"] * args.steps != segs_local:
+            print(f"[bench] work counters traced {work['segments']} segments, the timed frames "
+                  f"{segs_local / args.steps}", file=sys.stderr)
 
     verified = None
     if args.verify and rank == 0:
@@ -197,18 +207,28 @@ def main():
         samples = W * H * (params.spp if info.mode == wl.MODE_PATHTRACE else 1)
         if info.mode == wl.MODE_PATHTRACE:
             value = segs_all / elapsed_s / 1e6
-            flop_launch = (segs_local / steps) * info.flop_per_segment
-            achieved_tf = flop_launch / (k_ms * 1e-3) / 1e12
-            roof = {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4), "traffic": None,
+            seg_launch = segs_local / steps
+            brute_tf = seg_launch * info.flop_per_segment / (k_ms * 1e-3) / 1e12
+            roof = {"bound": "valu", "achieved": None, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": None,
+                    "traffic": None,
                     "kernel": {"jit": "wo_jit_pathtrace", "lanes": "pathtrace_lanes_kernel"}.get(r.trace_path(),
                                                                                               "pathtrace_kernel"),
-                    "kernel_ms": round(k_ms, 4),
-                    "flop_per_segment": info.flop_per_segment,
-                    "segments_per_launch": segs_local // steps, "trace_path": r.trace_path()}
-            if r.trace_path() == "lanes" or info.spheres + info.halfspaces > 64:
-                roof["note"] = ("flop_per_segment counts every primitive (SURVEY.md 8(d)); BOUND culling skips "
-                                "most of them here, so achieved/frac overstate the VALU work actually done")
+                    "kernel_ms": round(k_ms, 4), "segments_per_launch": segs_local // steps,
+                    "trace_path": r.trace_path(),
+                    "brute_force_flop_per_segment": info.flop_per_segment,
+                    "brute_force_achieved": round(brute_tf, 3),
+                    "brute_force_frac": round(brute_tf / PEAK_FP32_TFLOPS, 4)}
+            if work is not None:
+                ex = executed_flop(work, info, r.trace_path())
+                ex_tf = ex / work["segments"] * seg_launch / (k_ms * 1e-3) / 1e12
+                roof.update({"achieved": round(ex_tf, 3), "frac": round(ex_tf / PEAK_FP32_TFLOPS, 4),
+                             "basis": "executed work (counted tests priced per SURVEY.md 8(d))",
+                             "executed_flop_per_segment": round(ex / work["segments"], 2),
+                             "work_per_segment": {k: round(v / work["segments"], 4) for k, v in work.items()
+                                                  if k != "segments"}})
+            else:
+                roof.update({"achieved": roof["brute_force_achieved"], "frac": roof["brute_force_frac"],
+                             "basis": "brute force (every primitive on every segment, SURVEY.md 8(d))"})
         else:
             value = W * H * steps / elapsed_s / 1e6
             bytes_launch = lr * W * 16
@@ -255,6 +275,16 @@ def main():
         dist.destroy_process_group()
     if not verified_all:
         sys.exit(3)
+
+
+# SURVEY.md 8(d) prices: ray-sphere test 30 flop, ray-half-space 12, CSG combine 4 per
+# binop (one root evaluation per swept event; the lane tracer's union count is one
+# update), shading + scatter 40 per segment.  A BOUND test is the sphere test's
+# centre-to-line part without the root: priced 20.
+def executed_flop(work, info, path):
+    combine = 4 if path == "lanes" else 4 * info.binops
+    return (30 * work["sphere_tests"] + 12 * work["halfspace_tests"] + 20 * work["bound_tests"]
+            + combine * work["sweep_steps"] + 40 * work["segments"])
 
 
 def cpu_baseline(r, params, budget_s: float):

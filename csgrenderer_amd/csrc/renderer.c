@@ -544,6 +544,19 @@ int wo_renderer_render_rows_device(Wo_Renderer* r, Wo_RenderParams const* params
     return 0;
 }
 
+int wo_renderer_count_work(Wo_Renderer* r, Wo_RenderParams const* params, uint32_t tile_rows, uint32_t rank,
+                           uint32_t nranks, unsigned long long* counts) {
+    if (sync_device(r)) return -1;
+    WoFrame fr;
+    if (wo_renderer_frame_desc(r, params, tile_rows, rank, nranks, &fr)) return -1;
+    char err[256] = {0};
+    if (wo_dev_count_work(r->dev, &fr, counts, err, sizeof err)) {
+        wo_set_error("counting launch failed: %s", err);
+        return -1;
+    }
+    return 0;
+}
+
 int wo_assemble_rows_device(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,
                             uint32_t tile_rows, uint32_t nranks, void* stream) {
     char err[256] = {0};

@@ -118,7 +118,7 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
             for (int i = 0; i < 5; ++i) vb[i] = fbits(r->f[i]);
             uint32_t k = g->nbound++;
             if (g->first_pass) { /* the wave's cull decision; re-collects reuse it */
-                bput(g->b, "%*s{  // BOUND %u\n", indent, "", k);
+                bput(g->b, "%*s{  // BOUND %u\n%*s  WO_WK(WO_WORK_BOUND_TESTS);\n", indent, "", k, indent, "");
                 emit_consts(g->b, indent + 2, "float", nb, vb, 5);
                 bput(g->b,
                      "%*s  if (__ballot(wodev::bound_may_hit(bc0, bc1, bc2, bc3, bc4, o, d)) == 0ull) cull[%u] |= %uu;\n"
@@ -152,12 +152,15 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
                     const char ax = axis[L->u1 - 1u];
                     uint32_t vh[2] = {vl[3], fbits(L2->f[3])};
                     emit_consts(g->b, indent + 4, "float", nh, vh, 2);
+                    bput(g->b, "%*s    WO_WK_N(WO_WORK_HALFSPACE_TESTS, 2u);\n", indent, "");
                     if (m == 0) bput(g->b, "%*s    wodev::ivl_open(iv);\n", indent, "");
                     bput(g->b, "%*s    wodev::axis_pair_meet(iv, %s, c3, c3b, o.%c, d.%c, iv%c, %uu, %uu);\n%*s  }\n",
                          indent, "", L->f[L->u1 - 1u] > 0.0f ? "1.0f" : "-1.0f", ax, ax, ax, m, m + 1u, indent, "");
                     ++m;
                     continue;
                 }
+                bput(g->b, "%*s    WO_WK(%s);\n", indent, "",
+                     L->op == WO_LEAF_SPHERE ? "WO_WORK_SPHERE_TESTS" : "WO_WORK_HALFSPACE_TESTS");
                 if (L->op == WO_LEAF_HALFSPACE && L->u1 != 0u) {
                     /* axis-aligned: s = +-1 stays a literal (inline constant), h in an SGPR */
                     static const char* nh[1] = {"c3"};
@@ -188,15 +191,15 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
             if (g->first_pass)
                 bput(g->b,
                      "%*s    bits[%u] |= ((iv.a <= tmin && iv.b > tmin) ? 1u : 0u) << %u;\n"
-                     "%*s    if (iv.a > tmin) win.insert(wodev::event_key_lo(iv.a, ka | iv.ma));\n"
-                     "%*s    if ((iv.b > tmin) & (iv.b < wodev::kInf)) win.insert(wodev::event_key_lo(iv.b, kb | iv.mb));\n"
+                     "%*s    if (iv.a > tmin) { WO_WK(WO_WORK_EVENTS); win.insert(wodev::event_key_lo(iv.a, ka | iv.ma)); }\n"
+                     "%*s    if ((iv.b > tmin) & (iv.b < wodev::kInf)) { WO_WK(WO_WORK_EVENTS); win.insert(wodev::event_key_lo(iv.b, kb | iv.mb)); }\n"
                      "%*s  }\n%*s}\n",
                      indent, "", ord / 32, ord % 32, indent, "", indent, "", indent, "", indent, "");
             else
                 bput(g->b,
                      "%*s    uint64_t k0 = wodev::event_key_lo(iv.a, ka | iv.ma), k1 = wodev::event_key_lo(iv.b, kb | iv.mb);\n"
-                     "%*s    if ((iv.a > tmin) & (k0 > after)) win.insert(k0);\n"
-                     "%*s    if ((iv.b > tmin) & (iv.b < wodev::kInf) & (k1 > after)) win.insert(k1);\n"
+                     "%*s    if ((iv.a > tmin) & (k0 > after)) { WO_WK(WO_WORK_EVENTS); win.insert(k0); }\n"
+                     "%*s    if ((iv.b > tmin) & (iv.b < wodev::kInf) & (k1 > after)) { WO_WK(WO_WORK_EVENTS); win.insert(k1); }\n"
                      "%*s  }\n%*s}\n",
                      indent, "", indent, "", indent, "", indent, "", indent, "");
             pc += 1 + cnt;
@@ -510,6 +513,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     bput(&b, "};\n\n");
     bput(&b,
          "struct JitTracer {\n"
+         "  static constexpr bool kCount = WO_COUNT_WORK != 0;  // counting variant: -DWO_COUNT_WORK=1\n"
+         "  wodev::WorkCounts wk;\n"
          "  const WoRec* __restrict__ prog;\n"
          "  const uint32_t* __restrict__ ordpc;\n"
          "  uint64_t* ev;  // LDS event list column (LdsWindow)\n"
@@ -567,6 +572,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "      if (!win.next(key)) {  // key keeps the last processed event\n"
              "        if (!win.dropped()) return false;\n"
              "        after = key;\n"
+             "        WO_WK(WO_WORK_RECOLLECTS);\n"
              "        win.clear();\n"
              "        {\n");
         g.nbound = 0;
@@ -577,6 +583,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "        if (!win.next(key)) return false;\n"
              "      }\n"
              "      have = true;\n"
+             "      WO_WK(WO_WORK_SWEEP_STEPS);\n"
              "      {\n"
              "        uint32_t ord = ((uint32_t)key) >> 12;\n"
              "        uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n");

@@ -59,13 +59,14 @@ struct ProgPtr {
 
 // `inv`/`have_inv`: the ray's reciprocal direction, computed on the first
 // axis-aligned half-space met (wave-uniform condition).
-template <class Prog>
+template <bool kCount, class Prog>
 __device__ __forceinline__ Ivl prim_interval(Prog prog, uint32_t pc, uint32_t count, F3 o, F3 d, F3& inv,
-                                             bool& have_inv) {
+                                             bool& have_inv, WorkCounts& wk) {
     Ivl iv;
     for (uint32_t m = 0; m < count; ++m) {
         WoRec L = prog[pc + 1u + m];
         uint32_t kind = uni(L.op);
+        WO_WK(kind == WO_LEAF_SPHERE ? WO_WORK_SPHERE_TESTS : WO_WORK_HALFSPACE_TESTS);
         if (kind == WO_LEAF_HALFSPACE && !have_inv && uni(L.u1) != 0u) {
             inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
             have_inv = true;
@@ -81,7 +82,10 @@ __device__ __forceinline__ Ivl prim_interval(Prog prog, uint32_t pc, uint32_t co
 }
 
 // Interpreter: walks the program record by record (wave-uniform pc).
+template <bool kCountT>
 struct InterpTracer {
+    static constexpr bool kCount = kCountT;
+    WorkCounts wk;
     ProgPtr prog;
     uint32_t nrec;
     uint32_t* codes;
@@ -155,6 +159,7 @@ struct InterpTracer {
             uint32_t op = uni(rec.op);
             uint32_t code;
             if (op == WO_OP_BOUND) {
+                WO_WK(WO_WORK_BOUND_TESTS);
                 bool may = bound_may_hit(rec.f[0], rec.f[1], rec.f[2], rec.f[3], rec.f[4], o, d);
                 if (__ballot(may) != 0ull) {
                     ++pc;
@@ -166,12 +171,18 @@ struct InterpTracer {
             } else if (op == WO_OP_PRIM) {
                 uint32_t count = uni(rec.u0);
                 uint32_t ord = nprims;
-                Ivl iv = prim_interval(prog, pc, count, o, d, inv, have_inv);
+                Ivl iv = prim_interval<kCount>(prog, pc, count, o, d, inv, have_inv, wk);
                 uint32_t inside = 0;
                 if (!(iv.a > iv.b)) {
                     inside = (iv.a <= tmin && iv.b > tmin) ? 1u : 0u;
-                    if (iv.a > tmin) win.insert(event_key(iv.a, ord, 0u, iv.ma));
-                    if (iv.b > tmin && iv.b < kInf) win.insert(event_key(iv.b, ord, 1u, iv.mb));
+                    if (iv.a > tmin) {
+                        WO_WK(WO_WORK_EVENTS);
+                        win.insert(event_key(iv.a, ord, 0u, iv.ma));
+                    }
+                    if (iv.b > tmin && iv.b < kInf) {
+                        WO_WK(WO_WORK_EVENTS);
+                        win.insert(event_key(iv.b, ord, 1u, iv.mb));
+                    }
                 }
                 if (ord < 64u) {
                     bits |= (uint64_t)inside << ord;
@@ -210,6 +221,7 @@ struct InterpTracer {
         uint32_t root = st & 1u;
         while (win.k[0] != kEmptyKey) {
             uint64_t key = win.pop();
+            WO_WK(WO_WORK_SWEEP_STEPS);
             uint32_t ord = key_ord(key);
             toggle(ord);
             uint32_t r = eval_root();
@@ -221,6 +233,7 @@ struct InterpTracer {
             if (win.k[0] == kEmptyKey && win.dropped()) {
                 // window exhausted but events were dropped: re-collect the events
                 // strictly after `key` (the membership state carries on)
+                WO_WK(WO_WORK_RECOLLECTS);
                 win.clear();
                 uint32_t ordc = 0;
                 uint32_t nwords = (ncodes + 7u) >> 3;
@@ -232,15 +245,21 @@ struct InterpTracer {
                         if (((word >> (4u * j)) & 15u) != kCodePrim) continue;
                         uint32_t ppc = uni(ordpc[ordc]);
                         uint32_t count = uni(prog[ppc].u0);
-                        Ivl iv = prim_interval(prog, ppc, count, o, d, inv, have_inv);
+                        Ivl iv = prim_interval<kCount>(prog, ppc, count, o, d, inv, have_inv, wk);
                         if (!(iv.a > iv.b)) {
                             if (iv.a > tmin) {
                                 uint64_t k2 = event_key(iv.a, ordc, 0u, iv.ma);
-                                if (k2 > key) win.insert(k2);
+                                if (k2 > key) {
+                                    WO_WK(WO_WORK_EVENTS);
+                                    win.insert(k2);
+                                }
                             }
                             if (iv.b > tmin && iv.b < kInf) {
                                 uint64_t k2 = event_key(iv.b, ordc, 1u, iv.mb);
-                                if (k2 > key) win.insert(k2);
+                                if (k2 > key) {
+                                    WO_WK(WO_WORK_EVENTS);
+                                    win.insert(k2);
+                                }
                             }
                         }
                         ++ordc;
@@ -274,8 +293,10 @@ struct InterpTracer {
 // program.  20 bytes per node, staged in LDS when the table fits.
 constexpr uint32_t kNodeBound = 0u, kNodeSphere = 1u, kNodeGeneric = 2u;
 
-template <bool kLds>
+template <bool kLds, bool kCountT>
 struct LaneTracer {
+    static constexpr bool kCount = kCountT;
+    WorkCounts wk;
     const WoRec* __restrict__ prog;      // full program (generic primitives, hit leaves)
     const float4* geo;                   // LDS or global
     const uint32_t* aux;
@@ -307,6 +328,7 @@ struct LaneTracer {
                 float b, ll;
                 sphere_bl(g.x, g.y, g.z, o, d, b, ll);
                 if (kind == kNodeBound) {
+                    WO_WK(WO_WORK_BOUND_TESTS);
                     // tca = (c - o).d = -b; ll is the same bits either way
                     const float tca = -b, d2 = ll;
                     bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, g.w * g.w)) || (tca + g.w < 0.0f);
@@ -322,6 +344,7 @@ struct LaneTracer {
                 } else {
                     Ivl iv;
                     if (kind == kNodeSphere) {
+                        WO_WK(WO_WORK_SPHERE_TESTS);
                         float la, lb;
                         sphere_interval_bl(b, ll, g.w, la, lb);
                         ivl_first(iv, la, lb);
@@ -331,6 +354,7 @@ struct LaneTracer {
                         for (uint32_t m = 0; m < count; ++m) {
                             WoRec L = prog[ppc + 1u + m];
                             float la, lb;
+                            WO_WK(L.op == WO_LEAF_SPHERE ? WO_WORK_SPHERE_TESTS : WO_WORK_HALFSPACE_TESTS);
                             if (L.op == WO_LEAF_SPHERE) {
                                 sphere_interval(L.f[0], L.f[1], L.f[2], L.f[3], o, d, la, lb);
                             } else if (L.u1 != 0u) {
@@ -353,8 +377,14 @@ struct LaneTracer {
                     if (!(iv.a > iv.b)) {
                         if (first && iv.a <= tmin && iv.b > tmin) ++cnt;
                         uint64_t k0 = event_key(iv.a, val, 0u, iv.ma), k1 = event_key(iv.b, val, 1u, iv.mb);
-                        if (iv.a > tmin && k0 > after) win.insert(k0);
-                        if (iv.b > tmin && iv.b < kInf && k1 > after) win.insert(k1);
+                        if (iv.a > tmin && k0 > after) {
+                            WO_WK(WO_WORK_EVENTS);
+                            win.insert(k0);
+                        }
+                        if (iv.b > tmin && iv.b < kInf && k1 > after) {
+                            WO_WK(WO_WORK_EVENTS);
+                            win.insert(k1);
+                        }
                     }
                     ++pc;
                 }
@@ -373,6 +403,7 @@ struct LaneTracer {
                     break;
                 }
                 key = win.pop();
+                WO_WK(WO_WORK_SWEEP_STEPS);
                 cnt += (key & kKeyTypeBit) ? -1 : 1;
                 uint32_t rv = cnt > 0 ? 1u : 0u;
                 if (rv != root) {
@@ -382,6 +413,7 @@ struct LaneTracer {
                 root = rv;
             }
             if (!again) return false;
+            WO_WK(WO_WORK_RECOLLECTS);
             after = key;
         }
     }
@@ -390,12 +422,12 @@ struct LaneTracer {
 #ifndef WO_LANES_MIN_WAVES
 #define WO_LANES_MIN_WAVES 8  // rtiow_cover: 40.0 ms at 6, 37.4 at 7, 36.5 at 8 (64 VGPRs)
 #endif
-template <bool kLds>
+template <bool kLds, bool kCount>
 __global__ __launch_bounds__(kBlock, WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
     const WoRec* __restrict__ prog, const float4* __restrict__ gnodes, const uint32_t* __restrict__ ordpc,
     const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t ntrav, uint32_t local_rows, float4* __restrict__ out,
     unsigned long long* __restrict__ seg_slots, PathLaunch tg) {
-    LaneTracer<kLds> tr;
+    LaneTracer<kLds, kCount> tr;
     tr.prog = prog;
     tr.ordpc = ordpc;
     tr.ntrav = ntrav;
@@ -469,7 +501,7 @@ __global__ __launch_bounds__(kBlock) void ubershader_kernel(WoFrame fr, uint32_t
     out[(size_t)lrow * fr.width + lx] = res;
 }
 
-template <bool kProgInLds>
+template <bool kProgInLds, bool kCount>
 __global__ __launch_bounds__(kBlock) void pathtrace_kernel(const WoRec* __restrict__ gprog,
                                                            const WoMaterial* __restrict__ mats, WoFrame fr,
                                                            KLayout lay, uint32_t local_rows,
@@ -481,7 +513,7 @@ __global__ __launch_bounds__(kBlock) void pathtrace_kernel(const WoRec* __restri
     const uint32_t nrec = fr.n_recs;
 
     uint32_t* scratch = smem;
-    InterpTracer tr;
+    InterpTracer<kCount> tr;
     if constexpr (kProgInLds) {
         const uint4* src = reinterpret_cast<const uint4*>(gprog);
         uint4* dst = reinterpret_cast<uint4*>(smem);
@@ -517,6 +549,28 @@ __global__ __launch_bounds__(kBlock) void seg_collect_kernel(unsigned long long*
         unsigned long long t = 0;
         for (uint32_t w = 0; w < kBlock / 64u; ++w) t += part[w];
         if (t) atomicAdd(counter, t);
+    }
+}
+
+// Sums (and clears) the work counters of the segment slots (kinds 1..) into
+// out[kind] (counting launches).
+__global__ __launch_bounds__(kBlock) void work_collect_kernel(unsigned long long* __restrict__ slots,
+                                                              unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long part[WO_WORK_KINDS][kBlock / 64];
+    static_assert(kSegSlots == kBlock, "one slot per thread");
+    const uint32_t i = threadIdx.x;
+#pragma unroll
+    for (uint32_t k = 1; k < WO_WORK_KINDS; ++k) {
+        unsigned long long v = slots[i * kSegStride + k];
+        slots[i * kSegStride + k] = 0ull;
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if ((i & 63u) == 0u) part[k][i >> 6] = v;
+    }
+    __syncthreads();
+    if (i > 0u && i < WO_WORK_KINDS) {
+        unsigned long long t = 0;
+        for (uint32_t w = 0; w < kBlock / 64u; ++w) t += part[i][w];
+        out[i] = t;
     }
 }
 
@@ -585,6 +639,7 @@ struct WoDev {
     size_t ordpc_cap;
     uint32_t n_trav;
     unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
+    unsigned long long* d_work;      // WO_WORK_KINDS totals of a counting launch
     // progressive accumulation (3 int64 per pixel) and the draw_frame pipeline:
     // two frame slots, each a device frame, a pinned host copy and an event
     long long* d_accum;
@@ -614,6 +669,9 @@ struct WoDev {
     hipModule_t jit_module;
     hipFunction_t jit_fn;
     std::string jit_key;  // SHA-256 (hex) of the loaded code object's inputs
+    std::string jit_src;  // its source (the counting variant is built from it on demand)
+    hipModule_t count_module;
+    hipFunction_t count_fn;
     int jit_origin;       // 0 process cache, 1 disk cache, 2 compiled
     double jit_compile_sec;
 };
@@ -678,6 +736,7 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
     if (dev->d_trav) (void)hipFree(dev->d_trav);
     if (dev->d_ordpc) (void)hipFree(dev->d_ordpc);
     if (dev->d_segslots) (void)hipFree(dev->d_segslots);
+    if (dev->d_work) (void)hipFree(dev->d_work);
     if (dev->d_accum) (void)hipFree(dev->d_accum);
     for (int i = 0; i < 2; ++i) {
         if (dev->d_slot[i]) (void)hipFree(dev->d_slot[i]);
@@ -691,6 +750,7 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
         if (dev->part_ev[i]) (void)hipEventDestroy(dev->part_ev[i]);
     }
     if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
+    if (dev->count_module) (void)hipModuleUnload(dev->count_module);
     (void)hipStreamDestroy(dev->stream);
     delete dev;
 }
@@ -860,13 +920,16 @@ static std::vector<std::string> jit_extra_flags() {
     return out;
 }
 
-static std::vector<std::string> jit_options(const std::string& arch) {
+// `count`: the counting variant (executed-work counters, wo_dev_count_work)
+static std::vector<std::string> jit_options(const std::string& arch, bool count) {
     std::vector<std::string> opts = {"--offload-arch=" + arch, "-O3", "-ffp-contract=off", "-std=c++17"};
     for (const std::string& f : jit_extra_flags()) opts.push_back(f);
+    if (count) opts.push_back("-DWO_COUNT_WORK=1");
     return opts;
 }
 
-static int jit_compile(const char* src, const std::string& arch, std::vector<char>& code, char* err, size_t errlen) {
+static int jit_compile(const char* src, const std::string& arch, bool count, std::vector<char>& code, char* err,
+                       size_t errlen) {
     hiprtcProgram p;
     const char* hdr_src[] = {kEmbed_wo_device_common_h, kEmbed_wo_scene_h};
     const char* hdr_names[] = {"wo_device_common.h", "wololo/wo_scene.h"};
@@ -874,7 +937,7 @@ static int jit_compile(const char* src, const std::string& arch, std::vector<cha
         snprintf(err, errlen, "hiprtcCreateProgram failed");
         return -1;
     }
-    std::vector<std::string> opt_s = jit_options(arch);
+    std::vector<std::string> opt_s = jit_options(arch, count);
     std::vector<const char*> opts;
     for (const std::string& o : opt_s) opts.push_back(o.c_str());
     hiprtcResult rc = hiprtcCompileProgram(p, (int)opts.size(), opts.data());
@@ -898,7 +961,7 @@ static int jit_compile(const char* src, const std::string& arch, std::vector<cha
 // SHA-256 over everything the code object depends on: a format tag, the hiprtc
 // version, the target, the options (WOLOLO_JIT_FLAGS included), the embedded
 // headers and the generated source; each part length-prefixed.
-static std::string jit_key(const char* src, const std::string& arch) {
+static std::string jit_key(const char* src, const std::string& arch, bool count = false) {
     WoSha256 s;
     wo_sha256_init(&s);
     auto part = [&](const char* p, size_t n) {
@@ -912,7 +975,7 @@ static std::string jit_key(const char* src, const std::string& arch) {
     const int ver[2] = {vmaj, vmin};
     part((const char*)ver, sizeof ver);
     part(arch.data(), arch.size());
-    for (const std::string& o : jit_options(arch)) part(o.data(), o.size());
+    for (const std::string& o : jit_options(arch, count)) part(o.data(), o.size());
     part(kEmbed_wo_device_common_h, strlen(kEmbed_wo_device_common_h));
     part(kEmbed_wo_scene_h, strlen(kEmbed_wo_scene_h));
     part(src, strlen(src));
@@ -923,10 +986,10 @@ static std::string jit_key(const char* src, const std::string& arch) {
     return std::string(hex);
 }
 
-static int jit_code(const char* src, const std::string& arch, std::vector<char>& code, std::string& key, int& origin,
-                    double& seconds, char* err, size_t errlen) {
+static int jit_code(const char* src, const std::string& arch, bool count, std::vector<char>& code, std::string& key,
+                    int& origin, double& seconds, char* err, size_t errlen) {
     auto t0 = std::chrono::steady_clock::now();
-    key = jit_key(src, arch);
+    key = jit_key(src, arch, count);
     {
         std::lock_guard<std::mutex> lock(g_jit_mu);
         auto it = jit_cache().find(key);
@@ -943,7 +1006,7 @@ static int jit_code(const char* src, const std::string& arch, std::vector<char>&
             free(buf);
             origin = 1;
         } else {
-            if (jit_compile(src, arch, code, err, errlen)) return -1;
+            if (jit_compile(src, arch, count, code, err, errlen)) return -1;
             origin = 2;
             (void)wo_jit_disk_store(key.c_str(), code.data(), code.size());  // best effort
         }
@@ -960,11 +1023,29 @@ extern "C" long long wo_jit_code_object(const char* src, const char* arch, int* 
     std::string key;
     int org = -1;
     double sec = 0.0;
-    if (jit_code(src, arch ? std::string(arch) : std::string("gfx950"), code, key, org, sec, err, errlen)) return -1;
+    if (jit_code(src, arch ? std::string(arch) : std::string("gfx950"), false, code, key, org, sec, err, errlen))
+        return -1;
     if (origin) *origin = org;
     if (seconds) *seconds = sec;
     if (key_hex) snprintf(key_hex, 65, "%s", key.c_str());
     return (long long)code.size();
+}
+
+static int load_jit_module(const std::vector<char>& code, hipModule_t* mod, hipFunction_t* fn, char* err,
+                           size_t errlen) {
+    hipError_t e = hipModuleLoadData(mod, code.data());
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipModuleLoadData", e);
+        return -1;
+    }
+    e = hipModuleGetFunction(fn, *mod, "wo_jit_pathtrace");
+    if (e != hipSuccess) {
+        (void)hipModuleUnload(*mod);
+        *mod = nullptr;
+        set_err(err, errlen, "hipModuleGetFunction", e);
+        return -1;
+    }
+    return 0;
 }
 
 extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t errlen) {
@@ -973,11 +1054,15 @@ extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t err
         set_err(err, errlen, "hipSetDevice", e);
         return -1;
     }
+    if (dev->count_module) (void)hipModuleUnload(dev->count_module);  // built again on demand
+    dev->count_module = nullptr;
+    dev->count_fn = nullptr;
     if (!src) {  // disable
         if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
         dev->jit_module = nullptr;
         dev->jit_fn = nullptr;
         dev->jit_key.clear();
+        dev->jit_src.clear();
         dev->jit_origin = -1;
         return 0;
     }
@@ -986,24 +1071,15 @@ extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t err
     int origin = -1;
     double sec = 0.0;
     if (dev->jit_fn && dev->jit_key == jit_key(src, dev->arch)) return 0;
-    if (jit_code(src, dev->arch, code, key, origin, sec, err, errlen)) return -1;
+    if (jit_code(src, dev->arch, false, code, key, origin, sec, err, errlen)) return -1;
     hipModule_t mod = nullptr;
-    e = hipModuleLoadData(&mod, code.data());
-    if (e != hipSuccess) {
-        set_err(err, errlen, "hipModuleLoadData", e);
-        return -1;
-    }
     hipFunction_t fn = nullptr;
-    e = hipModuleGetFunction(&fn, mod, "wo_jit_pathtrace");
-    if (e != hipSuccess) {
-        (void)hipModuleUnload(mod);
-        set_err(err, errlen, "hipModuleGetFunction", e);
-        return -1;
-    }
+    if (load_jit_module(code, &mod, &fn, err, errlen)) return -1;
     if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
     dev->jit_module = mod;
     dev->jit_fn = fn;
     dev->jit_key = key;
+    dev->jit_src = src;
     dev->jit_origin = origin;
     dev->jit_compile_sec = sec;
     return 0;
@@ -1017,7 +1093,7 @@ extern "C" int wo_dev_jit_origin(WoDev* dev, double* seconds) {
 
 extern "C" int wo_jit_compile_check(const char* src, const char* arch, char* err, size_t errlen) {
     std::vector<char> code;
-    return jit_compile(src, arch ? std::string(arch) : std::string("gfx950"), code, err, errlen);
+    return jit_compile(src, arch ? std::string(arch) : std::string("gfx950"), false, code, err, errlen);
 }
 
 extern "C" int wo_dev_jit_active(WoDev* dev) { return dev && dev->jit_fn ? 1 : 0; }
@@ -1101,9 +1177,61 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
     return wo_dev_launch_ex(dev, frame_in, d_out, stream_v, d_segments, nullptr, 0u, err, errlen);
 }
 
+enum PathKind { kLanesLds, kLanesGlobal, kJit, kInterpLds, kInterpGlobal };
+
+template <bool kCount>
+static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
+    switch (kind) {
+    case kLanesLds:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<true, kCount>, kBlock, dyn_lds);
+    case kLanesGlobal:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<false, kCount>, kBlock, 0);
+    case kInterpLds:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_kernel<true, kCount>, kBlock, dyn_lds);
+    default:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_kernel<false, kCount>, kBlock, dyn_lds);
+    }
+}
+
+template <bool kCount>
+static void static_launch(PathKind kind, dim3 grid, size_t dyn_lds, hipStream_t stream, WoDev* dev, const WoFrame& fr,
+                          const KLayout& lay, uint32_t local_rows, float4* out, unsigned long long* slots,
+                          const PathLaunch& tg) {
+    switch (kind) {
+    case kLanesLds:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<true, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg);
+        break;
+    case kLanesGlobal:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<false, kCount>), grid, dim3(kBlock), 0, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg);
+        break;
+    case kInterpLds:
+        hipLaunchKernelGGL((pathtrace_kernel<true, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_mats, fr, lay, local_rows, out, slots, tg);
+        break;
+    default:
+        hipLaunchKernelGGL((pathtrace_kernel<false, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_mats, fr, lay, local_rows, out, slots, tg);
+        break;
+    }
+}
+
+static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* stream_v,
+                       unsigned long long* d_segments, long long* d_accum, uint32_t accum_spp, bool count, char* err,
+                       size_t errlen);
+
 extern "C" int wo_dev_launch_ex(WoDev* dev, WoFrame const* frame_in, void* d_out, void* stream_v,
                                 unsigned long long* d_segments, long long* d_accum, uint32_t accum_spp, char* err,
                                 size_t errlen) {
+    return launch_impl(dev, frame_in, d_out, stream_v, d_segments, d_accum, accum_spp, false, err, errlen);
+}
+
+// `count`: the counting variant of the chosen path kernel (work counters in the
+// segment slots; wo_dev_count_work collects them).
+static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* stream_v,
+                       unsigned long long* d_segments, long long* d_accum, uint32_t accum_spp, bool count, char* err,
+                       size_t errlen) {
     hipStream_t stream = (hipStream_t)stream_v;  // NULL = the null stream (HIP convention)
     WoFrame fr = *frame_in;
     if (fr.width == 0 || fr.height == 0) return 0;
@@ -1148,7 +1276,7 @@ extern "C" int wo_dev_launch_ex(WoDev* dev, WoFrame const* frame_in, void* d_out
             slots = dev->d_segslots;
         }
         // which kernel, with how much dynamic LDS; then the workgroups one CU holds
-        enum { kLanesLds, kLanesGlobal, kJit, kInterpLds, kInterpGlobal } kind;
+        PathKind kind;
         size_t dyn_lds = 0;
         KLayout lay = {};
         if (dev->lanes_on && dev->union_only && !dev->jit_fn) {
@@ -1177,21 +1305,11 @@ extern "C" int wo_dev_launch_ex(WoDev* dev, WoFrame const* frame_in, void* d_out
             }
         }
         int per_cu = 0;
-        switch (kind) {
-        case kLanesLds:
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pathtrace_lanes_kernel<true>, kBlock, dyn_lds);
-            break;
-        case kLanesGlobal:
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pathtrace_lanes_kernel<false>, kBlock, 0);
-            break;
-        case kJit: e = hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dev->jit_fn, kBlock, 0); break;
-        case kInterpLds:
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pathtrace_kernel<true>, kBlock, dyn_lds);
-            break;
-        default:
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pathtrace_kernel<false>, kBlock, dyn_lds);
-            break;
-        }
+        hipFunction_t jfn = count ? dev->count_fn : dev->jit_fn;
+        if (kind == kJit)
+            e = hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jfn, kBlock, 0);
+        else
+            e = count ? static_occupancy<true>(kind, dyn_lds, &per_cu) : static_occupancy<false>(kind, dyn_lds, &per_cu);
         if (e != hipSuccess || per_cu < 1) per_cu = 1;
         // a rank's local rows are bands of tile_rows consecutive frame rows: a tile
         // taller than a band would join rows far apart (incoherent primary rays)
@@ -1209,36 +1327,21 @@ extern "C" int wo_dev_launch_ex(WoDev* dev, WoFrame const* frame_in, void* d_out
             return -1;
         }
         dim3 grid((uint32_t)n_wg);
-        switch (kind) {
-        case kLanesLds:
-            hipLaunchKernelGGL(pathtrace_lanes_kernel<true>, grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                               dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg);
-            break;
-        case kLanesGlobal:
-            hipLaunchKernelGGL(pathtrace_lanes_kernel<false>, grid, dim3(kBlock), 0, stream, dev->d_prog, dev->d_trav,
-                               dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg);
-            break;
-        case kJit: {
+        if (kind == kJit) {
             const WoRec* p = dev->d_prog;
             const WoMaterial* m = dev->d_mats;
             unsigned long long* sl = slots;
             PathLaunch plv = tg;
             void* args[] = {&p, &m, &fr, &local_rows, &out, &sl, &plv};
-            e = hipModuleLaunchKernel(dev->jit_fn, grid.x, 1, 1, kBlock, 1, 1, 0, stream, args, nullptr);
+            e = hipModuleLaunchKernel(jfn, grid.x, 1, 1, kBlock, 1, 1, 0, stream, args, nullptr);
             if (e != hipSuccess) {
                 set_err(err, errlen, "hipModuleLaunchKernel", e);
                 return -1;
             }
-            break;
-        }
-        case kInterpLds:
-            hipLaunchKernelGGL(pathtrace_kernel<true>, grid, dim3(kBlock), dyn_lds, stream, dev->d_prog, dev->d_mats,
-                               fr, lay, local_rows, out, slots, tg);
-            break;
-        default:
-            hipLaunchKernelGGL(pathtrace_kernel<false>, grid, dim3(kBlock), dyn_lds, stream, dev->d_prog, dev->d_mats,
-                               fr, lay, local_rows, out, slots, tg);
-            break;
+        } else if (count) {
+            static_launch<true>(kind, grid, dyn_lds, stream, dev, fr, lay, local_rows, out, slots, tg);
+        } else {
+            static_launch<false>(kind, grid, dyn_lds, stream, dev, fr, lay, local_rows, out, slots, tg);
         }
         if (slots) hipLaunchKernelGGL(seg_collect_kernel, dim3(1), dim3(kBlock), 0, stream, slots, d_segments);
     } else {
@@ -1248,6 +1351,58 @@ extern "C" int wo_dev_launch_ex(WoDev* dev, WoFrame const* frame_in, void* d_out
     e = hipGetLastError();
     if (e != hipSuccess) {
         set_err(err, errlen, "kernel launch", e);
+        return -1;
+    }
+    return 0;
+}
+
+// One frame of this rank with the counting variant of its path kernel:
+// counts[WO_WORK_*] are lane counts of what ran (synchronous; the image goes to
+// the device's scratch frame and equals the normal kernel's).
+extern "C" int wo_dev_count_work(WoDev* dev, WoFrame const* frame, unsigned long long* counts, char* err,
+                                 size_t errlen) {
+    WoFrame fr = *frame;
+    if (fr.mode != WO_MODE_PATHTRACE && fr.mode != WO_MODE_NORMALS) {
+        snprintf(err, errlen, "work counters need a path-traced frame");
+        return -1;
+    }
+    hipError_t e = hipSetDevice(dev->device);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipSetDevice", e);
+        return -1;
+    }
+    if (dev->jit_fn && !dev->count_fn) {
+        std::vector<char> code;
+        std::string key;
+        int origin = -1;
+        double sec = 0.0;
+        if (jit_code(dev->jit_src.c_str(), dev->arch, true, code, key, origin, sec, err, errlen)) return -1;
+        if (load_jit_module(code, &dev->count_module, &dev->count_fn, err, errlen)) return -1;
+    }
+    const size_t local_rows = wo_rank_local_rows(fr.height, fr.tile_rows, fr.nranks);
+    if (ensure_buffer(&dev->d_frame, &dev->frame_cap, local_rows * fr.width * sizeof(float4), err, errlen)) return -1;
+    if (!dev->d_work) {
+        e = hipMalloc((void**)&dev->d_work, WO_WORK_KINDS * sizeof(unsigned long long));
+        if (e != hipSuccess) {
+            dev->d_work = nullptr;
+            set_err(err, errlen, "hipMalloc(work counters)", e);
+            return -1;
+        }
+    }
+    e = hipMemsetAsync(dev->d_work, 0, WO_WORK_KINDS * sizeof(unsigned long long), dev->stream);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipMemsetAsync(work counters)", e);
+        return -1;
+    }
+    if (launch_impl(dev, &fr, dev->d_frame, dev->stream, dev->d_work, nullptr, 0u, true, err, errlen)) return -1;
+    hipLaunchKernelGGL(work_collect_kernel, dim3(1), dim3(kBlock), 0, dev->stream, dev->d_segslots, dev->d_work);
+    e = hipGetLastError();
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(counts, dev->d_work, WO_WORK_KINDS * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           dev->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(dev->stream);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "work counters", e);
         return -1;
     }
     return 0;

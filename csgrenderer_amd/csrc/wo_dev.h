@@ -101,6 +101,9 @@ int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, uint32_t const**
 int wo_dev_srgb8(void const* d_rgba, void* d_bgra8, size_t pixels, void* stream, char* err, size_t errlen);
 /* present.c: the encode's 255 thresholds (host) */
 void wo_srgb8_thresholds(float out[255]);
+/* One frame of this rank's tiles with the counting variant of its path kernel
+ * (synchronous): counts[WO_WORK_KINDS] = lane counts of the work that ran. */
+int wo_dev_count_work(WoDev* dev, WoFrame const* frame, unsigned long long* counts, char* err, size_t errlen);
 /* Full frame into host memory (synchronous; owns a device frame buffer). */
 int wo_dev_render_host(WoDev* dev, WoFrame const* frame, float* host_rgba, char* err, size_t errlen);
 /* Un-interleave gathered rank buffers into a frame (async on `stream`). */

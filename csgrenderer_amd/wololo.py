@@ -27,6 +27,9 @@ MODE_UBERSHADER_RT1, MODE_DEBUG_ST, MODE_PATHTRACE, MODE_NORMALS = 0, 1, 2, 3
 TRACER_AUTO, TRACER_INTERPRETER, TRACER_JIT, TRACER_LANES = 0, 1, 2, 3
 TRACERS = {"auto": TRACER_AUTO, "interpreter": TRACER_INTERPRETER, "jit": TRACER_JIT, "lanes": TRACER_LANES}
 WO_T_MIN = 1.0e-3
+# wo_scene.h WO_WORK_* (executed-work counters)
+WORK_KINDS = ("segments", "sphere_tests", "halfspace_tests", "bound_tests", "events", "sweep_steps", "recollects",
+              "primary_segments")
 WO_NODE_INVALID = 0xFFFFFFFF
 
 
@@ -106,6 +109,8 @@ SIGNATURES = {
     "wo_renderer_render_f32": (c_int, [c_void_p, POINTER(RenderParams), c_void_p]),
     "wo_renderer_render_rows_device": (c_int, [c_void_p, POINTER(RenderParams), c_void_p, c_uint32, c_uint32,
                                                c_uint32, c_void_p, c_void_p]),
+    "wo_renderer_count_work": (c_int, [c_void_p, POINTER(RenderParams), c_uint32, c_uint32, c_uint32,
+                                       POINTER(c_ulonglong)]),
     "wo_assemble_rows_device": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_void_p]),
     "wo_renderer_set_devices": (c_int, [c_void_p, c_int]),
     "wo_renderer_device_count": (c_int, [c_void_p]),
@@ -371,6 +376,13 @@ class Renderer:
 
     def accumulated_spp(self) -> int:
         return int(self.lib.wo_renderer_accumulated_spp(self.ptr))
+
+    def count_work(self, params: RenderParams, tile_rows: int = 4, rank: int = 0, nranks: int = 1) -> dict:
+        """Executed-work counters of one frame (wo_renderer_count_work), by WORK_KINDS name."""
+        c = (c_ulonglong * len(WORK_KINDS))()
+        if self.lib.wo_renderer_count_work(self.ptr, ctypes.byref(params), tile_rows, rank, nranks, c):
+            raise WololoError(last_error())
+        return dict(zip(WORK_KINDS, (int(v) for v in c)))
 
     def render_rows_device(self, params: RenderParams, d_out: int, tile_rows: int, rank: int, nranks: int,
                            stream: int = 0, d_segments: int = 0):

@@ -74,6 +74,15 @@ int wo_renderer_render_rows_device(Wo_Renderer* r, Wo_RenderParams const* params
                                    uint32_t tile_rows, uint32_t rank, uint32_t nranks, void* stream,
                                    unsigned long long* d_segment_counter);
 
+/* Executed-work counters: render this rank's tiles once (synchronously, into
+ * scratch memory) with the counting variant of the path kernel the renderer
+ * runs -- same image, same segments -- and fill counts[WO_WORK_KINDS]
+ * (wo_scene.h: segments, sphere / half-space / BOUND tests, events stored,
+ * events swept, re-collects, primary segments; lane counts).  A measurement
+ * aid (the counting kernel is slower); PATHTRACE / NORMALS frames only. */
+int wo_renderer_count_work(Wo_Renderer* r, Wo_RenderParams const* params, uint32_t tile_rows, uint32_t rank,
+                           uint32_t nranks, unsigned long long* counts);
+
 /* Un-interleave nranks gathered local buffers (rank-major, each
  * wo_rank_local_rows(...) * width float4s) into a width*height float4 frame. */
 int wo_assemble_rows_device(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,

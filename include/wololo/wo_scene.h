@@ -115,6 +115,21 @@ typedef struct WoFrame {
     WoCamera cam;
 } WoFrame;
 
+/* Executed-work counters of a counting launch (wo_renderer_count_work): lane
+ * counts of what the path kernels actually ran, for the executed-work roofline
+ * (SURVEY.md 8(d) prices each kind). */
+enum {
+    WO_WORK_SEGMENTS = 0,        /* traced ray segments */
+    WO_WORK_SPHERE_TESTS = 1,    /* ray-sphere leaf intersections */
+    WO_WORK_HALFSPACE_TESTS = 2, /* ray-half-space leaf intersections */
+    WO_WORK_BOUND_TESTS = 3,     /* bounding-sphere (BOUND) tests */
+    WO_WORK_EVENTS = 4,          /* boundary events stored in the event window */
+    WO_WORK_SWEEP_STEPS = 5,     /* events swept (membership toggle + root evaluation) */
+    WO_WORK_RECOLLECTS = 6,      /* re-collect passes after a window overflow */
+    WO_WORK_PRIMARY = 7,         /* segments that are primary (camera) rays */
+    WO_WORK_KINDS = 8
+};
+
 /* Minimum ray parameter for every CSG segment (RTIOW's 0.001). */
 #define WO_T_MIN (1.0e-3f)
 
