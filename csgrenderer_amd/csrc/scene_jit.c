@@ -90,6 +90,7 @@ typedef struct Gen {
     int axis_pairs;   /* consecutive opposite faces on one axis fused (axis_pair_meet) */
     int bound_single; /* BOUND records around a single primitive tested too */
     int member_skip;  /* members after the first skipped when the interval is empty on every lane */
+    int pair_window;  /* LDS event list behind two register slots (PairLdsWindow) */
     int err;
 } Gen;
 
@@ -458,6 +459,12 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         const char* v = getenv("WOLOLO_JIT_LDS_EVENTS");
         if (v && *v) g.lds_events = v[0] != '0';
     }
+    /* LDS list behind two register slots (PairLdsWindow) */
+    g.pair_window = 1;
+    {
+        const char* v = getenv("WOLOLO_JIT_PAIR_WINDOW");
+        if (v && *v) g.pair_window = v[0] != '0';
+    }
     g.axis_pairs = 1;
     {
         const char* v = getenv("WOLOLO_JIT_AXIS_PAIRS");
@@ -515,6 +522,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "struct JitTracer {\n"
          "  static constexpr bool kCount = WO_COUNT_WORK != 0;  // counting variant: -DWO_COUNT_WORK=1\n"
          "  wodev::WorkCounts wk;\n"
+         "  uint64_t tmark;  // end of the first pass (section timing)\n"
          "  const WoRec* __restrict__ prog;\n"
          "  const uint32_t* __restrict__ ordpc;\n"
          "  uint64_t* ev;  // LDS event list column (LdsWindow)\n"
@@ -545,12 +553,14 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "    %s win; %swin.clear();\n"
              "    uint64_t after = 0ull, key = 0ull;\n"
              "    {\n",
-             g.lds_events ? "wodev::LdsWindow" : "wodev::Window", g.lds_events ? "win.ev = ev; " : "");
+             !g.lds_events ? "wodev::Window" : g.pair_window ? "wodev::PairLdsWindow" : "wodev::LdsWindow",
+             !g.lds_events ? "" : g.pair_window ? "win.rest.ev = ev; " : "win.ev = ev; ");
         g.nbound = 0;
         g.first_pass = 1;
         gen_collect(&g, 0, n_recs, 6);
         bput(&b,
              "    }\n"
+             "    WO_TMARK();\n"
              "    if (win.empty()) return false;\n"
              "    bool have = false;\n"
              "    uint32_t root = 0u;\n"

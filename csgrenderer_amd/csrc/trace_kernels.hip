@@ -22,7 +22,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -86,6 +88,7 @@ template <bool kCountT>
 struct InterpTracer {
     static constexpr bool kCount = kCountT;
     WorkCounts wk;
+    uint64_t tmark;  // section timing (counting builds)
     ProgPtr prog;
     uint32_t nrec;
     uint32_t* codes;
@@ -293,19 +296,203 @@ struct InterpTracer {
 // program.  20 bytes per node, staged in LDS when the table fits.
 constexpr uint32_t kNodeBound = 0u, kNodeSphere = 1u, kNodeGeneric = 2u;
 
-template <bool kLds, bool kCountT>
+// Ordered BVH traversal (the common case).  The host builds a binary AABB
+// hierarchy over the bounded primitives (build_lbvh; each node holds its two
+// children's boxes, expanded outward), and an `always` list of the unbounded
+// and outsized ones.  A lane walks it nearest child first with a short LDS
+// stack and prunes every box whose near end lies beyond the nearest entry event
+// found so far.  While the ray starts outside every primitive (none contains
+// the point at t_min), the first event in key order is an entry -- an exit
+// before any entry would need a primitive containing t_min -- and the root
+// (a union) flips there: the hit is the smallest entry key, which does not
+// depend on the visiting order, so the result is the general algorithm's bit for
+// bit.  A ray that starts inside some primitive (counted on the way: boxes that
+// contain the ray's start are never pruned) takes the general walk below.
+constexpr uint32_t kLeafRef = 0x80000000u, kNoRef = 0xffffffffu;
+constexpr uint32_t kLaneStack = 16;  // per-lane LDS stack entries (power of 2)
+
+// Slab test of a ray against an expanded AABB: [near, far] of the ray's overlap
+// (conservative: the boxes carry the slack; `ri` = reciprocal direction with
+// zero components replaced by +-1e30, `oi` = o * ri).
+__device__ __forceinline__ float box_near(float4 lo, float4 hi, F3 ri, F3 oi, float& far_t) {
+    const float ax = __builtin_fmaf(lo.x, ri.x, -oi.x), bx = __builtin_fmaf(hi.x, ri.x, -oi.x);
+    const float ay = __builtin_fmaf(lo.y, ri.y, -oi.y), by = __builtin_fmaf(hi.y, ri.y, -oi.y);
+    const float az = __builtin_fmaf(lo.z, ri.z, -oi.z), bz = __builtin_fmaf(hi.z, ri.z, -oi.z);
+    const float n = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    far_t = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    return n;
+}
+
+// kMode: 0 general walk over the table in LDS, 1 general walk over the table in
+// global memory, 2 ordered BVH.
+template <int kMode, bool kCountT>
 struct LaneTracer {
     static constexpr bool kCount = kCountT;
+    static constexpr bool kBvh = kMode == 2;
     WorkCounts wk;
+    uint64_t tmark;  // section timing (counting builds)
     const WoRec* __restrict__ prog;      // full program (generic primitives, hit leaves)
     const float4* geo;                   // LDS or global
     const uint32_t* aux;
     const uint32_t* __restrict__ ordpc;  // ordinal -> program pc
     uint32_t ntrav;
+    // ordered BVH (build_lbvh); lroot == kNoRef and nalways == 0: general walk only
+    const float4* __restrict__ lnodes;   // 4 float4 per node: childA lo|ref, childA hi|ref B, childB lo, childB hi
+    const float4* __restrict__ lgeo;     // per ordinal: sphere centre, r^2 (single-sphere primitives)
+    const uint32_t* __restrict__ lkind;  // per ordinal: 1 = single sphere, 0 = generic; then the always list
+    uint32_t nalways, lroot, nprims;
+    uint32_t* stk;                       // LDS stack column of this lane ([entry][lane])
 
     __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const { return prog[ordpc[h.ord] + 1u + h.member]; }
 
+    // Interval of primitive `ord` (the general walk's arithmetic, bit for bit).
+    __device__ __forceinline__ Ivl prim_ivl(uint32_t ord, F3 o, F3 d, F3& inv, bool& have_inv) {
+        Ivl iv;
+        if (lkind[ord] != 0u) {
+            WO_WK(WO_WORK_SPHERE_TESTS);
+            const float4 g = lgeo[ord];
+            float b, ll, la, lb;
+            sphere_bl(g.x, g.y, g.z, o, d, b, ll);
+            sphere_interval_bl(b, ll, g.w, la, lb);
+            ivl_first(iv, la, lb);
+        } else {
+            const uint32_t ppc = ordpc[ord];
+            const uint32_t count = prog[ppc].u0;
+            for (uint32_t m = 0; m < count; ++m) {
+                WoRec L = prog[ppc + 1u + m];
+                float la, lb;
+                WO_WK(L.op == WO_LEAF_SPHERE ? WO_WORK_SPHERE_TESTS : WO_WORK_HALFSPACE_TESTS);
+                if (L.op == WO_LEAF_SPHERE) {
+                    sphere_interval(L.f[0], L.f[1], L.f[2], L.f[3], o, d, la, lb);
+                } else if (L.u1 != 0u) {
+                    if (!have_inv) {
+                        inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                        have_inv = true;
+                    }
+                    uint32_t ax = L.u1 - 1u;
+                    halfspace_axis_interval(ax == 0u ? L.f[0] : (ax == 1u ? L.f[1] : L.f[2]), L.f[3], pick3(o, ax),
+                                            pick3(d, ax), pick3(inv, ax), la, lb);
+                } else {
+                    halfspace_interval(L.f[0], L.f[1], L.f[2], L.f[3], o, d, la, lb);
+                }
+                if (m == 0u)
+                    ivl_first(iv, la, lb);
+                else
+                    ivl_meet(iv, la, lb, m);
+            }
+        }
+        return iv;
+    }
+
+    // The smallest event key > `after` (entries and exits after t_min), or
+    // kEmptyKey; `inside` (first query only) counts the primitives whose
+    // interval holds t_min.  Boxes are pruned beyond the best event so far; the
+    // boxes holding the ray's start never are, so the count is complete.
+    __device__ __forceinline__ uint64_t query(F3 o, F3 d, F3 ri, F3 oi, uint64_t after, uint32_t& inside, F3& inv,
+                                              bool& have_inv) {
+        const float tmin = WO_T_MIN;
+        uint64_t best = kEmptyKey;
+        auto visit = [&](uint32_t ord, uint32_t& cnt) {
+            const Ivl iv = prim_ivl(ord, o, d, inv, have_inv);
+            if (!(iv.a > iv.b)) {
+                if (iv.a <= tmin && iv.b > tmin) ++cnt;
+                const uint64_t k0 = event_key(iv.a, ord, 0u, iv.ma), k1 = event_key(iv.b, ord, 1u, iv.mb);
+                if (iv.a > tmin && k0 > after) {
+                    WO_WK(WO_WORK_EVENTS);
+                    best = k0 < best ? k0 : best;
+                }
+                if (iv.b > tmin && iv.b < kInf && k1 > after) {
+                    WO_WK(WO_WORK_EVENTS);
+                    best = k1 < best ? k1 : best;
+                }
+            }
+        };
+        uint32_t in_always = 0, in_tree = 0;
+        for (uint32_t i = 0; i < nalways; ++i) visit(lkind[nprims + i], in_always);
+        uint32_t cur = lroot, sp = 0, bottom = 0;
+        bool lost = false;
+        while (cur != kNoRef) {
+            if (cur & kLeafRef) {
+                visit(cur & ~kLeafRef, in_tree);
+                cur = kNoRef;
+            } else {
+                WO_WK_N(WO_WORK_BOUND_TESTS, 2u);
+                const float4* nd = lnodes + 4u * cur;
+                const float4 a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                // useful range: up to the best event so far
+                const float tb = best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(best >> 32));
+                float fa, fb;
+                const float na = box_near(a0, a1, ri, oi, fa), nb = box_near(b0, b1, ri, oi, fb);
+                const bool ha = fa >= fmaxf(na, 0.0f) && na <= tb;
+                const bool hb = fb >= fmaxf(nb, 0.0f) && nb <= tb;
+                const uint32_t ra = __float_as_uint(a0.w), rb = __float_as_uint(a1.w);
+                if (ha && hb) {
+                    const bool a_first = na <= nb;
+                    cur = a_first ? ra : rb;
+                    const uint32_t other = a_first ? rb : ra;
+                    if (sp - bottom == kLaneStack) {  // full: drop the oldest, walk again later
+                        ++bottom;
+                        lost = true;
+                    }
+                    stk[(sp & (kLaneStack - 1u)) * kBlock] = other;
+                    ++sp;
+                } else {
+                    cur = ha ? ra : (hb ? rb : kNoRef);
+                }
+            }
+            if (cur == kNoRef) {
+                if (sp != bottom) {
+                    --sp;
+                    cur = stk[(sp & (kLaneStack - 1u)) * kBlock];
+                } else if (lost) {  // entries were dropped: walk again (the minimum is idempotent)
+                    lost = false;
+                    sp = bottom = 0;
+                    in_tree = 0;
+                    cur = lroot;
+                }
+            }
+        }
+        inside = in_always + in_tree;
+        return best;
+    }
+
+    // Events in key order, one query each, from the count of primitives holding
+    // t_min; the root (count > 0) flips at the hit.  A ray that starts outside
+    // every primitive needs one query: its first event is an entry.
+    __device__ __forceinline__ bool trace_ordered(F3 o, F3 d, Hit& hit) {
+        // culling arithmetic only: approximate reciprocals are fine (the boxes carry the slack)
+        const float dx = fabsf(d.x) < 1e-30f ? copysignf(1e-30f, d.x) : d.x;
+        const float dy = fabsf(d.y) < 1e-30f ? copysignf(1e-30f, d.y) : d.y;
+        const float dz = fabsf(d.z) < 1e-30f ? copysignf(1e-30f, d.z) : d.z;
+        const F3 ri = f3(__builtin_amdgcn_rcpf(dx), __builtin_amdgcn_rcpf(dy), __builtin_amdgcn_rcpf(dz));
+        const F3 oi = f3(o.x * ri.x, o.y * ri.y, o.z * ri.z);
+        F3 inv = f3(0.0f, 0.0f, 0.0f);
+        bool have_inv = false;
+        uint32_t cnt = 0, unused = 0;
+        uint64_t key = query(o, d, ri, oi, 0ull, cnt, inv, have_inv);
+        const uint32_t root = cnt > 0u ? 1u : 0u;
+        while (key != kEmptyKey) {
+            WO_WK(WO_WORK_SWEEP_STEPS);
+            cnt = (key & kKeyTypeBit) ? cnt - 1u : cnt + 1u;
+            const uint32_t rv = cnt > 0u ? 1u : 0u;
+            if (rv != root) {
+                hit_from_key(key, rv, hit);
+                return true;
+            }
+            WO_WK(WO_WORK_RECOLLECTS);
+            key = query(o, d, ri, oi, key, unused, inv, have_inv);
+        }
+        return false;
+    }
+
     __device__ __forceinline__ bool trace(F3 o, F3 d, Hit& hit) {
+        if constexpr (kBvh)
+            return trace_ordered(o, d, hit);
+        else
+            return trace_general(o, d, hit);
+    }
+
+    __device__ __forceinline__ bool trace_general(F3 o, F3 d, Hit& hit) {
         const float tmin = WO_T_MIN;
         F3 inv = f3(0.0f, 0.0f, 0.0f);
         bool have_inv = false;
@@ -422,20 +609,42 @@ struct LaneTracer {
 #ifndef WO_LANES_MIN_WAVES
 #define WO_LANES_MIN_WAVES 8  // rtiow_cover: 40.0 ms at 6, 37.4 at 7, 36.5 at 8 (64 VGPRs)
 #endif
-template <bool kLds, bool kCount>
-__global__ __launch_bounds__(kBlock, WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
+// The ordered-BVH tables of a union-only program (build_lbvh).
+struct LaneBvh {
+    const float4* nodes;
+    const float4* geo;
+    const uint32_t* kind;  // per ordinal, then the always list
+    uint32_t nalways, root, nprims;
+};
+
+// Dynamic LDS: the lane stacks ([kLaneStack][kBlock] u32), then (kLds) the
+// general walk's table.
+#ifndef WO_LANES_BVH_MIN_WAVES
+#define WO_LANES_BVH_MIN_WAVES 7  // rtiow_cover: 16.86 ms at 8, 16.63 at 7, 17.26 at 6
+#endif
+template <int kMode, bool kCount>
+__global__ __launch_bounds__(kBlock, kMode == 2 ? WO_LANES_BVH_MIN_WAVES : WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
     const WoRec* __restrict__ prog, const float4* __restrict__ gnodes, const uint32_t* __restrict__ ordpc,
     const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t ntrav, uint32_t local_rows, float4* __restrict__ out,
-    unsigned long long* __restrict__ seg_slots, PathLaunch tg) {
-    LaneTracer<kLds, kCount> tr;
+    unsigned long long* __restrict__ seg_slots, PathLaunch tg, LaneBvh bvh) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    constexpr bool kLds = kMode == 0;
+    LaneTracer<kMode, kCount> tr;
     tr.prog = prog;
     tr.ordpc = ordpc;
     tr.ntrav = ntrav;
+    tr.lnodes = bvh.nodes;
+    tr.lgeo = bvh.geo;
+    tr.lkind = bvh.kind;
+    tr.nalways = bvh.nalways;
+    tr.lroot = bvh.root;
+    tr.nprims = bvh.nprims;
+    tr.stk = smem + threadIdx.x;  // kMode 2 only
     const uint32_t* gaux = reinterpret_cast<const uint32_t*>(gnodes + ntrav);
     if constexpr (kLds) {
-        extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-        float4* lgeo = reinterpret_cast<float4*>(smem);
-        uint32_t* laux = smem + ntrav * 4u;
+        uint32_t* table = smem;
+        float4* lgeo = reinterpret_cast<float4*>(table);
+        uint32_t* laux = table + ntrav * 4u;
         for (uint32_t i = threadIdx.x; i < ntrav; i += kBlock) {
             lgeo[i] = gnodes[i];
             laux[i] = gaux[i];
@@ -638,6 +847,11 @@ struct WoDev {
     uint32_t* d_ordpc;
     size_t ordpc_cap;
     uint32_t n_trav;
+    // the lane tracer's ordered BVH (build_lbvh): [4 float4 per node][float4 per
+    // ordinal] then u32 [kind per ordinal][always list]
+    float4* d_lbvh;
+    size_t lbvh_cap;
+    uint32_t lb_nodes, lb_always, lb_root, lb_nprims;
     unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
     unsigned long long* d_work;      // WO_WORK_KINDS totals of a counting launch
     // progressive accumulation (3 int64 per pixel) and the draw_frame pipeline:
@@ -734,6 +948,7 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
     if (dev->d_mats) (void)hipFree(dev->d_mats);
     if (dev->d_frame) (void)hipFree(dev->d_frame);
     if (dev->d_trav) (void)hipFree(dev->d_trav);
+    if (dev->d_lbvh) (void)hipFree(dev->d_lbvh);
     if (dev->d_ordpc) (void)hipFree(dev->d_ordpc);
     if (dev->d_segslots) (void)hipFree(dev->d_segslots);
     if (dev->d_work) (void)hipFree(dev->d_work);
@@ -853,6 +1068,236 @@ static int build_trav(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     return 0;
 }
 
+// ---- the lane tracer's ordered BVH ----
+// Axis-aligned box of a convex primitive from its members (spheres, axis-aligned
+// half-spaces; general planes bound nothing), in double; false if unbounded or
+// empty.
+static bool prim_aabb(WoRec const* prog, uint32_t pc, double lo[3], double hi[3]) {
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = -INFINITY;
+        hi[a] = INFINITY;
+    }
+    for (uint32_t m = 0; m < prog[pc].u0; ++m) {
+        const WoRec& L = prog[pc + 1u + m];
+        if (L.op == WO_LEAF_SPHERE) {
+            const double r = sqrt((double)L.f[3]);
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = fmax(lo[a], (double)L.f[a] - r);
+                hi[a] = fmin(hi[a], (double)L.f[a] + r);
+            }
+        } else if (L.op == WO_LEAF_HALFSPACE && L.u1 >= 1u && L.u1 <= 3u) {
+            const int a = (int)L.u1 - 1;  // s * x_a <= h
+            if (L.f[a] > 0.0f)
+                hi[a] = fmin(hi[a], (double)L.f[3]);
+            else
+                lo[a] = fmax(lo[a], -(double)L.f[3]);
+        }
+    }
+    for (int a = 0; a < 3; ++a)
+        if (!std::isfinite(lo[a]) || !std::isfinite(hi[a]) || lo[a] > hi[a]) return false;
+    return true;
+}
+
+struct LbPrim {
+    double lo[3], hi[3], c[3];
+    uint32_t ord;
+};
+
+struct LbBox {
+    double lo[3], hi[3];
+    void empty() {
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = INFINITY;
+            hi[a] = -INFINITY;
+        }
+    }
+    void grow(const double* l, const double* h) {
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fmin(lo[a], l[a]);
+            hi[a] = fmax(hi[a], h[a]);
+        }
+    }
+    double area() const {
+        const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+        return x < 0.0 ? 0.0 : 2.0 * (x * y + y * z + z * x);
+    }
+};
+
+// Binned-SAH build over prims[b, e); returns the subtree's ref.  Node n is
+// written to nodes[4n..4n+3] as the two children's boxes (rounded outward to
+// float) with their refs in the .w of the first two.
+static uint32_t lb_build(std::vector<LbPrim>& prims, uint32_t b, uint32_t e, std::vector<float4>& nodes,
+                         LbBox& box_out) {
+    box_out.empty();
+    for (uint32_t i = b; i < e; ++i) box_out.grow(prims[i].lo, prims[i].hi);
+    if (e - b == 1u) return kLeafRef | prims[b].ord;
+    LbBox cb;
+    cb.empty();
+    for (uint32_t i = b; i < e; ++i) cb.grow(prims[i].c, prims[i].c);
+    int axis = 0;
+    for (int a = 1; a < 3; ++a)
+        if (cb.hi[a] - cb.lo[a] > cb.hi[axis] - cb.lo[axis]) axis = a;
+    uint32_t mid = b + (e - b) / 2u;
+    const double ext = cb.hi[axis] - cb.lo[axis];
+    if (ext > 0.0) {
+        constexpr int kBins = 16;
+        LbBox bb[kBins];
+        uint32_t bn[kBins] = {};
+        for (int k = 0; k < kBins; ++k) bb[k].empty();
+        auto bin_of = [&](const LbPrim& p) {
+            int k = (int)((p.c[axis] - cb.lo[axis]) / ext * kBins);
+            return k < 0 ? 0 : (k >= kBins ? kBins - 1 : k);
+        };
+        for (uint32_t i = b; i < e; ++i) {
+            const int k = bin_of(prims[i]);
+            bb[k].grow(prims[i].lo, prims[i].hi);
+            ++bn[k];
+        }
+        double best = INFINITY;
+        int split = -1;
+        for (int s = 1; s < kBins; ++s) {
+            LbBox l, r;
+            l.empty();
+            r.empty();
+            uint32_t nl = 0, nr = 0;
+            for (int k = 0; k < s; ++k) l.grow(bb[k].lo, bb[k].hi), nl += bn[k];
+            for (int k = s; k < kBins; ++k) r.grow(bb[k].lo, bb[k].hi), nr += bn[k];
+            if (!nl || !nr) continue;
+            const double cost = l.area() * nl + r.area() * nr;
+            if (cost < best) best = cost, split = s;
+        }
+        if (split > 0) {
+            auto it = std::partition(prims.begin() + b, prims.begin() + e,
+                                     [&](const LbPrim& p) { return bin_of(p) < split; });
+            mid = (uint32_t)(it - prims.begin());
+        }
+    }
+    if (mid == b || mid == e) {  // no useful split: the median along the axis
+        mid = b + (e - b) / 2u;
+        std::nth_element(prims.begin() + b, prims.begin() + mid, prims.begin() + e,
+                         [&](const LbPrim& x, const LbPrim& y) { return x.c[axis] < y.c[axis]; });
+    }
+    const uint32_t n = (uint32_t)(nodes.size() / 4u);
+    nodes.resize(nodes.size() + 4u);
+    LbBox lb, rb;
+    const uint32_t lref = lb_build(prims, b, mid, nodes, lb);
+    const uint32_t rref = lb_build(prims, mid, e, nodes, rb);
+    auto bits_f = [](uint32_t u) {
+        float f;
+        memcpy(&f, &u, sizeof f);
+        return f;
+    };
+    auto down = [](double v) { return nextafterf((float)v, -INFINITY); };
+    auto up = [](double v) { return nextafterf((float)v, INFINITY); };
+    float4* q = &nodes[4u * n];
+    q[0] = make_float4(down(lb.lo[0]), down(lb.lo[1]), down(lb.lo[2]), bits_f(lref));
+    q[1] = make_float4(up(lb.hi[0]), up(lb.hi[1]), up(lb.hi[2]), bits_f(rref));
+    q[2] = make_float4(down(rb.lo[0]), down(rb.lo[1]), down(rb.lo[2]), 0.0f);
+    q[3] = make_float4(up(rb.hi[0]), up(rb.hi[1]), up(rb.hi[2]), 0.0f);
+    return n;
+}
+
+// Union-only programs: an AABB BVH over the bounded primitives (boxes expanded by
+// 1e-4 of their size and position plus 1e-5, so the approximate slab test never
+// culls a primitive the exact arithmetic meets) and the always list: unbounded
+// primitives and outsized ones (box diagonal > 16x the median, e.g. an RTIOW
+// ground sphere, which every ray meets anyway).  WOLOLO_LANES_BVH=0: none (the
+// general walk only).
+static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n_prims, char* err, size_t errlen) {
+    dev->lb_nodes = dev->lb_always = 0;
+    dev->lb_root = kNoRef;
+    dev->lb_nprims = n_prims;
+    const char* env = getenv("WOLOLO_LANES_BVH");
+    if (!dev->union_only || (env && env[0] == '0')) return 0;
+    std::vector<LbPrim> prims;
+    std::vector<uint32_t> always;
+    std::vector<float4> geo(n_prims, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    std::vector<uint32_t> kind(n_prims, 0u);
+    for (uint32_t pc = 0; pc < n_recs;) {
+        const WoRec& r = prog[pc];
+        if (r.op != WO_OP_PRIM) {
+            ++pc;
+            continue;
+        }
+        const uint32_t ord = r.u1;
+        if (ord >= n_prims) {
+            snprintf(err, errlen, "primitive ordinal out of range");
+            return -1;
+        }
+        const WoRec& L = prog[pc + 1u];
+        if (r.u0 == 1u && L.op == WO_LEAF_SPHERE) {
+            geo[ord] = make_float4(L.f[0], L.f[1], L.f[2], L.f[3]);
+            kind[ord] = 1u;
+        }
+        LbPrim p;
+        p.ord = ord;
+        if (prim_aabb(prog, pc, p.lo, p.hi)) {
+            for (int a = 0; a < 3; ++a) {
+                const double m = 1e-4 * (fabs(p.lo[a]) + fabs(p.hi[a]) + (p.hi[a] - p.lo[a])) + 1e-5;
+                p.lo[a] -= m;
+                p.hi[a] += m;
+                p.c[a] = 0.5 * (p.lo[a] + p.hi[a]);
+            }
+            prims.push_back(p);
+        } else {
+            always.push_back(ord);
+        }
+        pc += 1u + r.u0;
+    }
+    if (!prims.empty()) {
+        std::vector<double> diag(prims.size());
+        for (size_t i = 0; i < prims.size(); ++i) {
+            double s = 0.0;
+            for (int a = 0; a < 3; ++a) s += (prims[i].hi[a] - prims[i].lo[a]) * (prims[i].hi[a] - prims[i].lo[a]);
+            diag[i] = sqrt(s);
+        }
+        std::vector<double> sorted = diag;
+        std::nth_element(sorted.begin(), sorted.begin() + sorted.size() / 2, sorted.end());
+        const double med = sorted[sorted.size() / 2];
+        std::vector<LbPrim> kept;
+        for (size_t i = 0; i < prims.size(); ++i) {
+            if (prims.size() > 4u && diag[i] > 16.0 * med)
+                always.push_back(prims[i].ord);
+            else
+                kept.push_back(prims[i]);
+        }
+        prims.swap(kept);
+    }
+    std::vector<float4> nodes;
+    if (!prims.empty()) {
+        LbBox root_box;
+        dev->lb_root = lb_build(prims, 0u, (uint32_t)prims.size(), nodes, root_box);
+    }
+    dev->lb_nodes = (uint32_t)(nodes.size() / 4u);
+    dev->lb_always = (uint32_t)always.size();
+    const size_t f4 = nodes.size() + n_prims;
+    const size_t bytes = f4 * sizeof(float4) + ((size_t)n_prims + always.size()) * sizeof(uint32_t);
+    if (ensure_buffer(&dev->d_lbvh, &dev->lbvh_cap, bytes, err, errlen)) return -1;
+    std::vector<char> blob(bytes);
+    memcpy(blob.data(), nodes.data(), nodes.size() * sizeof(float4));
+    memcpy(blob.data() + nodes.size() * sizeof(float4), geo.data(), n_prims * sizeof(float4));
+    memcpy(blob.data() + f4 * sizeof(float4), kind.data(), n_prims * sizeof(uint32_t));
+    memcpy(blob.data() + f4 * sizeof(float4) + n_prims * sizeof(uint32_t), always.data(),
+           always.size() * sizeof(uint32_t));
+    hipError_t e = hipMemcpy(dev->d_lbvh, blob.data(), bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipMemcpy(lane BVH)", e);
+        return -1;
+    }
+    return 0;
+}
+
+static LaneBvh lane_bvh(const WoDev* dev) {
+    LaneBvh b;
+    b.nodes = dev->d_lbvh;
+    b.geo = dev->d_lbvh + 4u * dev->lb_nodes;
+    b.kind = reinterpret_cast<const uint32_t*>(dev->d_lbvh + 4u * dev->lb_nodes + dev->lb_nprims);
+    b.nalways = dev->lb_always;
+    b.root = dev->lb_root;
+    b.nprims = dev->lb_nprims;
+    return b;
+}
+
 extern "C" int wo_dev_upload_scene(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n_prims,
                                    WoMaterial const* mats, uint32_t n_mats, char* err, size_t errlen) {
     hipError_t e = hipSetDevice(dev->device);
@@ -888,7 +1333,8 @@ extern "C" int wo_dev_upload_scene(WoDev* dev, WoRec const* prog, uint32_t n_rec
     dev->n_recs = n_recs;
     dev->n_prims = n_prims;
     dev->n_mats = n_mats;
-    return build_trav(dev, prog, n_recs, n_prims, err, errlen);
+    if (build_trav(dev, prog, n_recs, n_prims, err, errlen)) return -1;
+    return build_lbvh(dev, prog, n_recs, n_prims, err, errlen);
 }
 
 // ---- scene-specialised kernels (hiprtc) ----
@@ -1177,15 +1623,17 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
     return wo_dev_launch_ex(dev, frame_in, d_out, stream_v, d_segments, nullptr, 0u, err, errlen);
 }
 
-enum PathKind { kLanesLds, kLanesGlobal, kJit, kInterpLds, kInterpGlobal };
+enum PathKind { kLanesLds, kLanesGlobal, kLanesBvh, kJit, kInterpLds, kInterpGlobal };
 
 template <bool kCount>
 static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
     switch (kind) {
     case kLanesLds:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<true, kCount>, kBlock, dyn_lds);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<0, kCount>, kBlock, dyn_lds);
     case kLanesGlobal:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<false, kCount>, kBlock, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<1, kCount>, kBlock, dyn_lds);
+    case kLanesBvh:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<2, kCount>, kBlock, dyn_lds);
     case kInterpLds:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_kernel<true, kCount>, kBlock, dyn_lds);
     default:
@@ -1199,12 +1647,19 @@ static void static_launch(PathKind kind, dim3 grid, size_t dyn_lds, hipStream_t 
                           const PathLaunch& tg) {
     switch (kind) {
     case kLanesLds:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<true, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg);
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<0, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
         break;
     case kLanesGlobal:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<false, kCount>), grid, dim3(kBlock), 0, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg);
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<1, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesBvh:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<2, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
         break;
     case kInterpLds:
         hipLaunchKernelGGL((pathtrace_kernel<true, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
@@ -1280,9 +1735,16 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
         size_t dyn_lds = 0;
         KLayout lay = {};
         if (dev->lanes_on && dev->union_only && !dev->jit_fn) {
-            dyn_lds = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
-            kind = dyn_lds <= kLanesLdsBudget ? kLanesLds : kLanesGlobal;
-            if (kind == kLanesGlobal) dyn_lds = 0;
+            // the ordered BVH: the lane stacks in LDS; the general walk: its table
+            // in LDS when it fits
+            const size_t table = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
+            if (dev->lb_root != kNoRef || dev->lb_always != 0u) {
+                kind = kLanesBvh;
+                dyn_lds = (size_t)kLaneStack * kBlock * sizeof(uint32_t);
+            } else {
+                kind = table <= kLanesLdsBudget ? kLanesLds : kLanesGlobal;
+                dyn_lds = kind == kLanesLds ? table : 0u;
+            }
         } else if (dev->jit_fn) {
             kind = kJit;
         } else {

@@ -127,7 +127,14 @@ enum {
     WO_WORK_SWEEP_STEPS = 5,     /* events swept (membership toggle + root evaluation) */
     WO_WORK_RECOLLECTS = 6,      /* re-collect passes after a window overflow */
     WO_WORK_PRIMARY = 7,         /* segments that are primary (camera) rays */
-    WO_WORK_KINDS = 8
+    /* wave cycles per section of the path loop, summed over waves: only in a
+     * counting build with -DWO_TIME_SECTIONS=1 (WOLOLO_JIT_FLAGS), else 0 */
+    WO_WORK_CYC_TAKE = 8,        /* job queue + sample set-up */
+    WO_WORK_CYC_COLLECT = 9,     /* trace: first pass (culling, intervals, events) */
+    WO_WORK_CYC_SWEEP = 10,      /* trace: sweep + re-collects */
+    WO_WORK_CYC_SHADE = 11,      /* hit shading, scatter, accumulation */
+    WO_WORK_CYC_LOOP = 12,       /* whole loop iterations */
+    WO_WORK_KINDS = 13
 };
 
 /* Minimum ray parameter for every CSG segment (RTIOW's 0.001). */
