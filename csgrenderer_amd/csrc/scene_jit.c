@@ -459,8 +459,10 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         const char* v = getenv("WOLOLO_JIT_LDS_EVENTS");
         if (v && *v) g.lds_events = v[0] != '0';
     }
-    /* LDS list behind two register slots (PairLdsWindow) */
-    g.pair_window = 1;
+    /* LDS list behind two register slots (PairLdsWindow): slower (csg32 4.69 ->
+     * 4.92 ms, csg256 balanced 13.99 -> 14.75): the two u64 slots spill at the
+     * 64-VGPR budget */
+    g.pair_window = 0;
     {
         const char* v = getenv("WOLOLO_JIT_PAIR_WINDOW");
         if (v && *v) g.pair_window = v[0] != '0';

@@ -824,7 +824,75 @@ __global__ __launch_bounds__(kBlock) void srgb8_kernel(const float4* __restrict_
     }
 }
 
+// Exhaustive check of sqrt_cr / rcp_cr over float bit patterns [lo, lo + count)
+// against the definition of correct rounding, evaluated exactly in double
+// (independent of any library expansion): s = RN(sqrt x) iff (s - u/2)^2 <= x
+// <= (s + u/2)^2, u = ulp(s) (the squares of 25-bit numbers are exact in double,
+// and no float x sits on a midpoint); r = RN(1/x) iff |1 - r x| <= (u/2) |x|,
+// u = ulp(r) (r x is exact in double).  Counts the patterns that fail.
+__global__ __launch_bounds__(kBlock) void fastmath_check_kernel(uint32_t lo, uint32_t count, int which,
+                                                                unsigned long long* __restrict__ bad,
+                                                                uint32_t* __restrict__ first_bad) {
+    unsigned long long nbad = 0;
+    uint32_t first = 0xffffffffu;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < count; i += gridDim.x * kBlock) {
+        const uint32_t u = lo + i;
+        const float x = __uint_as_float(u);
+        bool ok;
+        if (which == 0) {
+            const float s = sqrt_cr(x);
+            const double sd = s, h = 0.5 * ((double)__uint_as_float(__float_as_uint(s) + 1u) - sd);
+            ok = (sd - h) * (sd - h) <= (double)x && (double)x <= (sd + h) * (sd + h);
+        } else {
+            const float r = rcp_cr(x);
+            const double rd = r, h = 0.5 * ((double)__uint_as_float(__float_as_uint(r) + 1u) - rd);
+            ok = fabs(1.0 - rd * (double)x) <= h * fabs((double)x);
+        }
+        if (!ok) {
+            ++nbad;
+            first = u < first ? u : first;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) nbad += __shfl_xor(nbad, off, 64);
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)first, off, 64);
+        first = o < first ? o : first;
+    }
+    if ((threadIdx.x & 63u) == 0u) {
+        if (nbad) atomicAdd(bad, nbad);
+        if (first != 0xffffffffu) atomicMin(first_bad, first);
+    }
+}
+
 }  // namespace
+
+extern "C" int wo_fastmath_check(int which, uint32_t lo_bits, uint32_t hi_bits, unsigned long long* mismatches,
+                                 uint32_t* first_mismatch) {
+    unsigned long long* d_bad = nullptr;
+    uint32_t* d_first = nullptr;
+    if (hi_bits < lo_bits) return -1;
+    if (hipMalloc((void**)&d_bad, sizeof *d_bad) != hipSuccess) return -1;
+    if (hipMalloc((void**)&d_first, sizeof *d_first) != hipSuccess) {
+        (void)hipFree(d_bad);
+        return -1;
+    }
+    const uint32_t init = 0xffffffffu;
+    hipError_t e = hipMemset(d_bad, 0, sizeof *d_bad);
+    if (e == hipSuccess) e = hipMemcpy(d_first, &init, sizeof init, hipMemcpyHostToDevice);
+    const uint64_t total = (uint64_t)hi_bits - lo_bits + 1u;
+    for (uint64_t done = 0; e == hipSuccess && done < total;) {
+        const uint32_t n = (uint32_t)(total - done < (1ull << 30) ? total - done : (1ull << 30));
+        hipLaunchKernelGGL(fastmath_check_kernel, dim3(8192), dim3(kBlock), 0, nullptr, (uint32_t)(lo_bits + done), n,
+                           which, d_bad, d_first);
+        e = hipGetLastError();
+        done += n;
+    }
+    if (e == hipSuccess) e = hipMemcpy(mismatches, d_bad, sizeof *d_bad, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(first_mismatch, d_first, sizeof *d_first, hipMemcpyDeviceToHost);
+    (void)hipFree(d_bad);
+    (void)hipFree(d_first);
+    return e == hipSuccess ? 0 : -1;
+}
 
 // ===========================================================================
 // Host glue (C ABI declared in wo_dev.h)

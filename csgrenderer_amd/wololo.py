@@ -145,6 +145,7 @@ SIGNATURES = {
     "wo_version": (c_char_p, []),
     "wo_abi_layout": (c_size_t, [c_char_p, c_char_p]),
     "wo_hip_device_count": (c_int, []),
+    "wo_fastmath_check": (c_int, [c_int, c_uint32, c_uint32, POINTER(c_ulonglong), POINTER(c_uint32)]),
 }
 
 _lib = None
@@ -161,6 +162,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
                            f"g.build()'` or `make -C csgrenderer_amd/csrc`")
     lib = ctypes.CDLL(p)
     for name, (res, args) in SIGNATURES.items():
+        if os.environ.get("WOLOLO_LIB") and not hasattr(lib, name):
+            continue  # an older build under A/B measurement: bind what it has
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -214,6 +214,12 @@ void wo_renderer_clear_error(void);
  * Wo_Node_Argument, Wo_RenderParams, WoRec, WoMaterial, WoCamera, WoFrame);
  * (size_t)-1 for an unknown name.  Bindings check their mirrors with it. */
 size_t wo_abi_layout(char const* type, char const* field);
+/* Device self-check of the path tracer's fast correctly rounded square root
+ * (which = 0) or reciprocal (1) against the IEEE expansions, over every float
+ * bit pattern in [lo_bits, hi_bits] (on the current HIP device, synchronous).
+ * 0 and the mismatch count / smallest mismatching pattern, or -1. */
+int wo_fastmath_check(int which, uint32_t lo_bits, uint32_t hi_bits, unsigned long long* mismatches,
+                      uint32_t* first_mismatch);
 char const* wo_version(void);
 /* Number of visible HIP devices (0 when none / no driver). */
 int wo_hip_device_count(void);

@@ -133,9 +133,12 @@ uint32_t oracle_rng_next(uint32_t* state) {
 static float rng_float(uint32_t* state) { return (float)(oracle_rng_next(state) >> 8) * (1.0f / 16777216.0f); }
 
 static float dot3(const float a[3], const float b[3]) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+/* The path tracer's square root: sqrtf of max(x, 2^-96) (wo_device_common.h
+ * sqrt_pt; the kernels' correctly rounded sequence is exact from 2^-96 up). */
+static float sqrt_pt(float x) { return sqrtf(fmaxf(x, 0x1p-96f)); }
 
 static void normalize3(float v[3]) {
-    float inv = 1.0f / sqrtf(dot3(v, v));
+    float inv = 1.0f / sqrt_pt(dot3(v, v));
     v[0] = v[0] * inv;
     v[1] = v[1] * inv;
     v[2] = v[2] * inv;
@@ -174,7 +177,7 @@ static void sincos_turn(float u, float* s, float* c) {
 /* Uniform unit vector: z uniform in [-1, 1], azimuth uniform. */
 static void rand_unit_vector(uint32_t* rng, float p[3]) {
     float z = 1.0f - 2.0f * rng_float(rng);
-    float r = sqrtf(1.0f - z * z);
+    float r = sqrt_pt(1.0f - z * z);
     float s, c;
     sincos_turn(rng_float(rng), &s, &c);
     p[0] = r * c;
@@ -196,7 +199,7 @@ static void leaf_span(const WoRec* L, const float o[3], const float d[3], float*
             *hi = -INFINITY;
             return;
         }
-        float s = sqrtf(disc);
+        float s = sqrt_pt(disc);
         *lo = -b - s;
         *hi = -b + s;
         return;
@@ -467,7 +470,7 @@ static void shade_pixel(const WoRec* prog, uint32_t n, const WoMaterial* mats, u
         float off[3] = {0.0f, 0.0f, 0.0f};
         if (cam->lens_radius > 0.0f && !normals) {
             /* point on the unit disk: radius sqrt(u), angle 2*pi*v */
-            float rad = sqrtf(rng_float(&rng));
+            float rad = sqrt_pt(rng_float(&rng));
             float s, c;
             sincos_turn(rng_float(&rng), &s, &c);
             float px = rad * c, py = rad * s;
@@ -542,7 +545,7 @@ static void shade_pixel(const WoRec* prog, uint32_t n, const WoMaterial* mats, u
                 float nd0[3] = {-d[0], -d[1], -d[2]};
                 float ct = dot3(nd0, N);
                 if (!(ct < 1.0f)) ct = 1.0f;
-                float st = sqrtf(1.0f - ct * ct);
+                float st = sqrt_pt(1.0f - ct * ct);
                 int reflect = ri * st > 1.0f;
                 if (!reflect) {
                     const float r0 = m->r0; /* Schlick base, symmetric in ri and 1/ri */
@@ -557,7 +560,7 @@ static void shade_pixel(const WoRec* prog, uint32_t n, const WoMaterial* mats, u
                 } else {
                     float perp[3];
                     for (int i = 0; i < 3; ++i) perp[i] = ri * (d[i] + ct * N[i]);
-                    float par = -sqrtf(fabsf(1.0f - dot3(perp, perp)));
+                    float par = -sqrt_pt(fabsf(1.0f - dot3(perp, perp)));
                     for (int i = 0; i < 3; ++i) sc[i] = perp[i] + par * N[i];
                 }
                 memcpy(nd, sc, sizeof nd);

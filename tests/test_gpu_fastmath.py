@@ -1,0 +1,23 @@
+"""GPU: the path tracer's fast square root and reciprocal (wo_device_common.h
+sqrt_cr / rcp_cr) equal the IEEE correctly rounded results for every float in
+the ranges the kernels feed them -- checked exhaustively on the device against
+the definition of correct rounding evaluated exactly in double, so the oracle
+can state them as sqrtf / '/' (with the same clamp at 2^-96).""" 
+import ctypes
+
+import pytest
+
+from csgrenderer_amd import wololo as wl
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("which,lo,hi", [
+    (0, 0x0F800000, 0x7F7FFFFF),  # sqrt: [2^-96, max float]
+    (1, 0x1F800000, 0x5F800000),  # reciprocal: [2^-64, 2^64]
+])
+def test_fast_cr_math_is_exact(which, lo, hi):
+    bad = ctypes.c_ulonglong(0)
+    first = ctypes.c_uint32(0)
+    assert wl.load().wo_fastmath_check(which, lo, hi, ctypes.byref(bad), ctypes.byref(first)) == 0
+    assert bad.value == 0, f"{bad.value} mismatches, first at bits 0x{first.value:08x}"
