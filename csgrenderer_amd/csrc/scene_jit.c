@@ -541,7 +541,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         for (uint32_t i = 0; i < n_recs; ++i)
             if (prog[i].op == WO_LEAF_HALFSPACE && prog[i].u1 >= 1u && prog[i].u1 <= 3u) axes |= 1u << (prog[i].u1 - 1u);
         for (int a = 0; a < 3; ++a)
-            if (axes & (1u << a)) bput(&b, "    const float iv%c = 1.0f / d.%c;\n", "xyz"[a], "xyz"[a]);
+            if (axes & (1u << a)) bput(&b, "    const float iv%c = wodev::rcp_dir(d.%c);\n", "xyz"[a], "xyz"[a]);
         bput(&b, "    uint32_t bits[%u];\n", nw);
         for (uint32_t w = 0; w < nw; ++w) bput(&b, "    bits[%u] = 0u;\n", w);
         uint32_t ncw = nbounds ? (nbounds + 31u) / 32u : 1u;

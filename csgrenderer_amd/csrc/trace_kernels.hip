@@ -845,7 +845,7 @@ __global__ __launch_bounds__(kBlock) void fastmath_check_kernel(uint32_t lo, uin
             ok = (sd - h) * (sd - h) <= (double)x && (double)x <= (sd + h) * (sd + h);
         } else {
             const float r = rcp_cr(x);
-            const double rd = r, h = 0.5 * ((double)__uint_as_float(__float_as_uint(r) + 1u) - rd);
+            const double rd = r, h = 0.5 * fabs((double)__uint_as_float(__float_as_uint(r) + 1u) - rd);
             ok = fabs(1.0 - rd * (double)x) <= h * fabs((double)x);
         }
         if (!ok) {

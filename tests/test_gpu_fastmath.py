@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("which,lo,hi", [
     (0, 0x0F800000, 0x7F7FFFFF),  # sqrt: [2^-96, max float]
     (1, 0x1F800000, 0x5F800000),  # reciprocal: [2^-64, 2^64]
+    (1, 0x9F800000, 0xDF800000),  # reciprocal: [-2^64, -2^-64]
 ])
 def test_fast_cr_math_is_exact(which, lo, hi):
     bad = ctypes.c_ulonglong(0)
