@@ -91,6 +91,7 @@ typedef struct Gen {
     int bound_single; /* BOUND records around a single primitive tested too */
     int member_skip;  /* members after the first skipped when the interval is empty on every lane */
     int pair_window;  /* LDS event list behind two register slots (PairLdsWindow) */
+    int lit_spheres;  /* sphere constants as VALU literal operands instead of scalar moves */
     int err;
 } Gen;
 
@@ -171,6 +172,19 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
                     bput(g->b,
                          "%*s    wodev::halfspace_axis_interval(%s, c3, o.%c, d.%c, iv%c, la, lb);\n",
                          indent, "", L->f[L->u1 - 1u] > 0.0f ? "1.0f" : "-1.0f", ax, ax, ax);
+                } else if (L->op == WO_LEAF_SPHERE && g->lit_spheres) {
+                    /* the centre and r^2 as VALU literal operands: o - c and r^2 - ll
+                     * are single VOP2 operations (the constant needs no scalar move) */
+                    bput(g->b,
+                         "%*s    float fx, fy, fz, b, ll, disc;\n"
+                         "%*s    asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fx) : \"v\"(o.x));\n"
+                         "%*s    asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fy) : \"v\"(o.y));\n"
+                         "%*s    asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fz) : \"v\"(o.z));\n"
+                         "%*s    wodev::sphere_fbl(fx, fy, fz, d, b, ll);\n"
+                         "%*s    asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(disc) : \"v\"(ll));\n"
+                         "%*s    wodev::sphere_interval_bd(b, disc, la, lb);\n",
+                         indent, "", indent, "", vl[0], indent, "", vl[1], indent, "", vl[2], indent, "", indent, "",
+                         vl[3], indent, "");
                 } else {
                     emit_consts(g->b, indent + 4, "float", nl, vl, 4);
                     bput(g->b,
@@ -467,6 +481,11 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         const char* v = getenv("WOLOLO_JIT_PAIR_WINDOW");
         if (v && *v) g.pair_window = v[0] != '0';
     }
+    g.lit_spheres = 1;
+    {
+        const char* v = getenv("WOLOLO_JIT_LIT_SPHERES");
+        if (v && *v) g.lit_spheres = v[0] != '0';
+    }
     g.axis_pairs = 1;
     {
         const char* v = getenv("WOLOLO_JIT_AXIS_PAIRS");
@@ -554,6 +573,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         bput(&b,
              "    %s win; %swin.clear();\n"
              "    uint64_t after = 0ull, key = 0ull;\n"
+             "    WO_MARK(\"collect_begin\");\n"
              "    {\n",
              !g.lds_events ? "wodev::Window" : g.pair_window ? "wodev::PairLdsWindow" : "wodev::LdsWindow",
              !g.lds_events ? "" : g.pair_window ? "win.rest.ev = ev; " : "win.ev = ev; ");
@@ -562,6 +582,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         gen_collect(&g, 0, n_recs, 6);
         bput(&b,
              "    }\n"
+             "    WO_MARK(\"collect_end\");\n"
              "    WO_TMARK();\n"
              "    if (win.empty()) return false;\n"
              "    bool have = false;\n"
