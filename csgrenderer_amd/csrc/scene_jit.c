@@ -91,7 +91,7 @@ typedef struct Gen {
     int bound_single; /* BOUND records around a single primitive tested too */
     int member_skip;  /* members after the first skipped when the interval is empty on every lane */
     int pair_window;  /* LDS event list behind two register slots (PairLdsWindow) */
-    int lit_spheres;  /* sphere constants as VALU literal operands instead of scalar moves */
+    int lit_consts;   /* sphere / BOUND / axis-face constants as VALU literal operands instead of scalar moves */
     int err;
 } Gen;
 
@@ -121,11 +121,30 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
             uint32_t k = g->nbound++;
             if (g->first_pass) { /* the wave's cull decision; re-collects reuse it */
                 bput(g->b, "%*s{  // BOUND %u\n%*s  WO_WK(WO_WORK_BOUND_TESTS);\n", indent, "", k, indent, "");
-                emit_consts(g->b, indent + 2, "float", nb, vb, 5);
-                bput(g->b,
-                     "%*s  if (__ballot(wodev::bound_may_hit(bc0, bc1, bc2, bc3, bc4, o, d)) == 0ull) cull[%u] |= %uu;\n"
-                     "%*s}\n",
-                     indent, "", k / 32, 1u << (k % 32), indent, "");
+                if (g->lit_consts) {
+                    /* c - o and tca + R with the constants as VALU literal operands; R^2
+                     * (an FMA addend) in an SGPR */
+                    static const char* nr[1] = {"bc3"};
+                    emit_consts(g->b, indent + 2, "float", nr, &vb[3], 1);
+                    bput(g->b,
+                         "%*s  float ox, oy, oz, tca, d2, tr;\n"
+                         "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(ox) : \"v\"(o.x));\n"
+                         "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oy) : \"v\"(o.y));\n"
+                         "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oz) : \"v\"(o.z));\n"
+                         "%*s  wodev::bound_tca_d2(ox, oy, oz, d, tca, d2);\n"
+                         "%*s  asm(\"v_add_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(tr) : \"v\"(tca));\n"
+                         "%*s  const bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, bc3)) || (tr < 0.0f);\n"
+                         "%*s  if (__ballot(!miss) == 0ull) cull[%u] |= %uu;\n"
+                         "%*s}\n",
+                         indent, "", indent, "", vb[0], indent, "", vb[1], indent, "", vb[2], indent, "", indent, "",
+                         vb[4], indent, "", indent, "", k / 32, 1u << (k % 32), indent, "");
+                } else {
+                    emit_consts(g->b, indent + 2, "float", nb, vb, 5);
+                    bput(g->b,
+                         "%*s  if (__ballot(wodev::bound_may_hit(bc0, bc1, bc2, bc3, bc4, o, d)) == 0ull) cull[%u] |= %uu;\n"
+                         "%*s}\n",
+                         indent, "", k / 32, 1u << (k % 32), indent, "");
+                }
             }
             bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
             gen_collect(g, pc + 1, r->u0, indent + 2);
@@ -152,12 +171,26 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
                     static const char* nh[2] = {"c3", "c3b"};
                     static const char axis[3] = {'x', 'y', 'z'};
                     const char ax = axis[L->u1 - 1u];
+                    const int pos = L->f[L->u1 - 1u] > 0.0f; /* s1 = +1 */
                     uint32_t vh[2] = {vl[3], fbits(L2->f[3])};
-                    emit_consts(g->b, indent + 4, "float", nh, vh, 2);
                     bput(g->b, "%*s    WO_WK_N(WO_WORK_HALFSPACE_TESTS, 2u);\n", indent, "");
                     if (m == 0) bput(g->b, "%*s    wodev::ivl_open(iv);\n", indent, "");
-                    bput(g->b, "%*s    wodev::axis_pair_meet(iv, %s, c3, c3b, o.%c, d.%c, iv%c, %uu, %uu);\n%*s  }\n",
-                         indent, "", L->f[L->u1 - 1u] > 0.0f ? "1.0f" : "-1.0f", ax, ax, ax, m, m + 1u, indent, "");
+                    if (g->lit_consts) {
+                        /* dist1 = h1 - s1*oa, dist2 = h2 + s1*oa with h as a literal operand */
+                        bput(g->b,
+                             "%*s    float dist1, dist2;\n"
+                             "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist1) : \"v\"(o.%c));\n"
+                             "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist2) : \"v\"(o.%c));\n"
+                             "%*s    wodev::axis_pair_meet_d(iv, %s, dist1, dist2, d.%c, iv%c, %uu, %uu);\n%*s  }\n",
+                             indent, "", indent, "", pos ? "v_sub_f32_e32" : "v_add_f32_e32", vh[0], ax, indent, "",
+                             pos ? "v_add_f32_e32" : "v_sub_f32_e32", vh[1], ax, indent, "", pos ? "1.0f" : "-1.0f", ax,
+                             ax, m, m + 1u, indent, "");
+                    } else {
+                        emit_consts(g->b, indent + 4, "float", nh, vh, 2);
+                        bput(g->b,
+                             "%*s    wodev::axis_pair_meet(iv, %s, c3, c3b, o.%c, d.%c, iv%c, %uu, %uu);\n%*s  }\n",
+                             indent, "", pos ? "1.0f" : "-1.0f", ax, ax, ax, m, m + 1u, indent, "");
+                    }
                     ++m;
                     continue;
                 }
@@ -168,11 +201,21 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
                     static const char* nh[1] = {"c3"};
                     static const char axis[3] = {'x', 'y', 'z'};
                     char ax = axis[L->u1 - 1u];
-                    emit_consts(g->b, indent + 4, "float", nh, &vl[3], 1);
-                    bput(g->b,
-                         "%*s    wodev::halfspace_axis_interval(%s, c3, o.%c, d.%c, iv%c, la, lb);\n",
-                         indent, "", L->f[L->u1 - 1u] > 0.0f ? "1.0f" : "-1.0f", ax, ax, ax);
-                } else if (L->op == WO_LEAF_SPHERE && g->lit_spheres) {
+                    const int pos = L->f[L->u1 - 1u] > 0.0f;
+                    if (g->lit_consts) {
+                        bput(g->b,
+                             "%*s    float dist;\n"
+                             "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist) : \"v\"(o.%c));\n"
+                             "%*s    wodev::halfspace_axis_dist(%s, dist, d.%c, iv%c, la, lb);\n",
+                             indent, "", indent, "", pos ? "v_sub_f32_e32" : "v_add_f32_e32", vl[3], ax, indent, "",
+                             pos ? "1.0f" : "-1.0f", ax, ax);
+                    } else {
+                        emit_consts(g->b, indent + 4, "float", nh, &vl[3], 1);
+                        bput(g->b,
+                             "%*s    wodev::halfspace_axis_interval(%s, c3, o.%c, d.%c, iv%c, la, lb);\n",
+                             indent, "", pos ? "1.0f" : "-1.0f", ax, ax, ax);
+                    }
+                } else if (L->op == WO_LEAF_SPHERE && g->lit_consts) {
                     /* the centre and r^2 as VALU literal operands: o - c and r^2 - ll
                      * are single VOP2 operations (the constant needs no scalar move) */
                     bput(g->b,
@@ -481,10 +524,12 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         const char* v = getenv("WOLOLO_JIT_PAIR_WINDOW");
         if (v && *v) g.pair_window = v[0] != '0';
     }
-    g.lit_spheres = 1;
+    /* constants as VALU literals (csg32 4.46 -> 4.38 ms, csg256 balanced 13.48 ->
+     * 13.01, chain 26.27 -> 25.27 for the spheres alone) */
+    g.lit_consts = 1;
     {
-        const char* v = getenv("WOLOLO_JIT_LIT_SPHERES");
-        if (v && *v) g.lit_spheres = v[0] != '0';
+        const char* v = getenv("WOLOLO_JIT_LIT_CONSTS");
+        if (v && *v) g.lit_consts = v[0] != '0';
     }
     g.axis_pairs = 1;
     {
