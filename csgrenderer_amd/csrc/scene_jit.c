@@ -92,6 +92,7 @@ typedef struct Gen {
     int member_skip;  /* members after the first skipped when the interval is empty on every lane */
     int pair_window;  /* LDS event list behind two register slots (PairLdsWindow) */
     int lit_consts;   /* sphere / BOUND / axis-face constants as VALU literal operands instead of scalar moves */
+    int first_event;  /* the first event of waves that start outside every primitive from a constant table */
     int err;
 } Gen;
 
@@ -465,6 +466,32 @@ static Term gen_eval_flat(Gen* g, uint32_t start, uint32_t end, int indent) {
     return stack[0];
 }
 
+/* The root's membership when only primitive p holds the point: the postfix
+ * program evaluated over bits = {p} (BOUND records do not change values). */
+static int single_root(const WoRec* prog, uint32_t n_recs, uint32_t p) {
+    uint8_t st[512];
+    uint32_t sp = 0;
+    for (uint32_t pc = 0; pc < n_recs;) {
+        const WoRec* r = &prog[pc];
+        if (r->op == WO_OP_PRIM) {
+            if (sp == sizeof st) return -1;
+            st[sp++] = r->u1 == p;
+            pc += 1u + r->u0;
+            continue;
+        }
+        if (r->op != WO_OP_BOUND) {
+            if (sp < 2u) return -1;
+            const uint8_t B = st[--sp], A = st[sp - 1u];
+            st[sp - 1u] = r->op == WO_OP_UNION   ? (A | B)
+                          : r->op == WO_OP_INTER ? (A & B)
+                          : r->op == WO_OP_DIFF  ? (A & !B)
+                                                 : (B & !A);
+        }
+        ++pc;
+    }
+    return sp == 1u ? st[0] : -1;
+}
+
 /* Depth of the CSG tree over primitives (a primitive is depth 0). */
 static uint32_t tree_depth(const WoRec* prog, uint32_t n_recs) {
     uint32_t stack[256];
@@ -530,6 +557,11 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     {
         const char* v = getenv("WOLOLO_JIT_LIT_CONSTS");
         if (v && *v) g.lit_consts = v[0] != '0';
+    }
+    g.first_event = n_prims <= 64u * 32u;
+    {
+        const char* v = getenv("WOLOLO_JIT_FIRST_EVENT");
+        if (v && *v) g.first_event = v[0] != '0' && g.first_event;
     }
     g.axis_pairs = 1;
     {
@@ -631,7 +663,37 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "    WO_TMARK();\n"
              "    if (win.empty()) return false;\n"
              "    bool have = false;\n"
-             "    uint32_t root = 0u;\n"
+             "    uint32_t root = 0u;\n");
+        if (g.first_event) {
+            /* Waves whose lanes all start outside every primitive: the root is 0 at
+             * t_min (the operators keep the empty set empty), the first event is an
+             * entry, and the root after it is a per-primitive constant (single_root):
+             * two evaluations saved when it flips. */
+            uint32_t sr[64] = {0};
+            for (uint32_t p = 0; p < n_prims && p < 64u * 32u; ++p) {
+                int v = single_root(prog, n_recs, p);
+                if (v < 0) g.err = 1;
+                if (v > 0) sr[p / 32u] |= 1u << (p % 32u);
+            }
+            bput(&b, "    if (__ballot((bits[0]");
+            for (uint32_t w = 1; w < nw; ++w) bput(&b, " | bits[%u]", w);
+            bput(&b,
+                 ") != 0u) == 0ull) {\n"
+                 "      win.next(key);\n"
+                 "      WO_WK(WO_WORK_SWEEP_STEPS);\n"
+                 "      const uint32_t ord = ((uint32_t)key) >> 12;\n"
+                 "      const uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n"
+                 "      uint32_t single = 0u;\n");
+            for (uint32_t w = 0; w < nw; ++w) {
+                bput(&b, "      bits[%u] ^= w == %uu ? m : 0u;\n", w, w);
+                if (sr[w]) bput(&b, "      single |= w == %uu ? (0x%08xu & m) : 0u;\n", w, sr[w]);
+            }
+            bput(&b,
+                 "      if (single != 0u) { wodev::hit_from_key(key, 1u, hit); return true; }\n"
+                 "      have = true;  // root stays 0\n"
+                 "    }\n");
+        }
+        bput(&b,
              "    for (;;) {\n"
              "      uint32_t r;\n"
              "      {\n");
