@@ -225,7 +225,7 @@ def main():
                              "basis": "executed work (counted tests priced per SURVEY.md 8(d))",
                              "executed_flop_per_segment": round(ex / work["segments"], 2),
                              "work_per_segment": {k: round(v / work["segments"], 4) for k, v in work.items()
-                                                  if k != "segments"}})
+                                                  if k != "segments" and not k.startswith("cyc_")}})
             else:
                 roof.update({"achieved": roof["brute_force_achieved"], "frac": roof["brute_force_frac"],
                              "basis": "brute force (every primitive on every segment, SURVEY.md 8(d))"})
