@@ -19,14 +19,15 @@ def test_csg32_source_compiles_for_gfx950(hostonly):
     # each of the two collect passes (first pass, re-collect), one cull flag per
     # BOUND, ordinal table of every primitive
     nleaf = sum(1 for i in range(nrec) if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE))
-    nsingle = len(re.findall(r"wodev::(sphere|halfspace|halfspace_axis)_interval\(", src))
-    npair = len(re.findall(r"wodev::axis_pair_meet\(", src))
+    # (a sphere with literal constants ends in sphere_interval_bd, an axis face in halfspace_axis_dist)
+    nsingle = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
+    npair = len(re.findall(r"wodev::axis_pair_meet(_d)?\(", src))
     assert npair >= 2 * 6  # the slab and the cube: three face pairs each, in both passes
     assert nsingle + 2 * npair == 2 * nleaf
     # the slab and the cube are axis-aligned: tagged by the compiler, emitted on the fast path
     naxis = sum(1 for i in range(nrec) if prog[i].op == wl.WO_LEAF_HALFSPACE and prog[i].u1 != 0)
     assert naxis >= 12
-    assert len(re.findall(r"wodev::halfspace_axis_interval\(", src)) + 2 * npair == 2 * naxis
+    assert len(re.findall(r"wodev::halfspace_axis_(interval|dist)\(", src)) + 2 * npair == 2 * naxis
     # wave-level tests only for BOUND subtrees of >= 6 leaves (scene_jit.c, WOLOLO_JIT_BOUND_MIN_LEAVES)
     # and not around a lone primitive (WOLOLO_JIT_BOUND_SINGLE=0: its member skip is the cheaper test)
     def lone(i):
@@ -34,7 +35,7 @@ def test_csg32_source_compiles_for_gfx950(hostonly):
 
     nb = sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND and prog[i].u1 >= 6 and not lone(i))
     assert 0 < nb < sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND)
-    assert len(re.findall(r"if \(__ballot\(wodev::bound_may_hit\(", src)) == nb
+    assert len(re.findall(r"if \(__ballot\((wodev::bound_may_hit\(|!miss\) == 0ull)", src)) == nb
     m = re.search(r"kOrdPc\[(\d+)\] = \{([^}]*)\}", src)
     assert int(m.group(1)) == nprim
     pcs = [int(x.strip().rstrip("u")) for x in m.group(2).split(",")]
@@ -52,7 +53,8 @@ def test_literals_round_trip(hostonly):
     r.union(wl.arg(s, (1.0 / 3.0, 2.0 / 7.0, -1e-7)), wl.arg(h, (0.1, 0.2, 0.3)))
     prog, nrec, _ = r.program()
     src = r.jit_source()
-    imms = {int(x, 16) for x in re.findall(r"s_mov_b32 %\d, 0x([0-9a-f]{8})", src)}
+    # scalar moves, or literal operands of the VALU instructions that use them
+    imms = {int(x, 16) for x in re.findall(r"(?:s_mov_b32 %\d|v_\w+ %0), 0x([0-9a-f]{8})", src)}
     for i in range(nrec):
         if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE):
             # axis-aligned half-spaces carry only h as an SGPR constant (s is a literal)
@@ -79,8 +81,8 @@ def test_member_skip_guards(hostonly, monkeypatch):
     scenes.build("csg32", r)
     prog, nrec, _ = r.program()
     src = r.jit_source()
-    pair_members = len(re.findall(r"wodev::axis_pair_meet\(", src))  # a pair is one member step
-    singles = len(re.findall(r"wodev::(sphere|halfspace|halfspace_axis)_interval\(", src))
+    pair_members = len(re.findall(r"wodev::axis_pair_meet(_d)?\(", src))  # a pair is one member step
+    singles = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
     nprims_emitted = 2 * sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_PRIM)
     assert src.count(guard) == singles + pair_members - nprims_emitted > 0
     monkeypatch.setenv("WOLOLO_JIT_MEMBER_SKIP", "0")
