@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N>1: gather each frame before the next renders (default: frame k+1 renders while frame k "
                          "is gathered, with either backend)")
+    ap.add_argument("--frames-in-flight", type=int, default=1,
+                    help="render streams / buffers: frame k+1 may start while frame k's last tiles finish")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 checks the assembled frame against a single full-frame render (bit-exact)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -107,8 +109,10 @@ def main():
     # the same two-buffer / two-stream / event code runs on either backend, so a gloo
     # rehearsal on one GPU executes what the RCCL run on 8 GPUs does
     pipelined = world > 1 and not args.no_pipeline
-    # two render buffers when pipelined: frame k+1 renders while frame k is gathered
-    outs = [torch.empty((lr, W, 4), dtype=torch.float32, device=dev) for _ in range(2 if pipelined else 1)]
+    # two render buffers when pipelined: frame k+1 renders while frame k is gathered; with F frames
+    # in flight, F buffers and F render streams
+    nbuf = max(args.frames_in_flight, 2 if pipelined else 1)
+    outs = [torch.empty((lr, W, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     seg = torch.zeros(1, dtype=torch.int64, device=dev)
     stacked = gathered = frame = None
     if world > 1 and rank == 0:
@@ -117,7 +121,11 @@ def main():
         gathered = list(stacked.unbind(0))
         frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
     cs = torch.cuda.current_stream(dev)  # gather + assemble (RCCL's stream follows it)
-    rs = torch.cuda.Stream(dev) if pipelined else cs  # render
+    # render streams (one per buffer when frames overlap)
+    if args.frames_in_flight > 1:
+        rss = [torch.cuda.Stream(dev) for _ in range(nbuf)]
+    else:
+        rss = [torch.cuda.Stream(dev) if pipelined else cs] * nbuf
     k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     k_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     rendered = [torch.cuda.Event() for _ in outs]
@@ -128,6 +136,7 @@ def main():
         b = frame_no[0] % len(outs)
         frame_no[0] += 1
         out = outs[b]
+        rs = rss[b]
         if released[b] is not None:
             rs.wait_event(released[b])
         if i is not None:

@@ -748,8 +748,8 @@ __global__ __launch_bounds__(kBlock) void seg_collect_kernel(unsigned long long*
     __shared__ unsigned long long part[kBlock / 64];
     unsigned long long v = 0;
     for (uint32_t i = threadIdx.x; i < kSegSlots; i += kBlock) {
-        v += slots[i * kSegStride];
-        slots[i * kSegStride] = 0ull;
+        // read and clear in one atomic: a kernel of another stream may be adding
+        v += atomicExch(&slots[i * kSegStride], 0ull);
     }
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     if ((threadIdx.x & 63u) == 0u) part[threadIdx.x >> 6] = v;

@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--stream-frames", type=int, default=0,
+                    help="also time this many back-to-back frames of each share alternating over two streams "
+                         "(frames in flight: a frame's first tiles start while the previous frame's last finish)")
     args = ap.parse_args()
 
     import torch
@@ -61,6 +64,21 @@ def main():
                 b.record(s)
                 b.synchronize()
                 ms.append(a.elapsed_time(b))
+            if args.stream_frames:
+                ss = [torch.cuda.Stream(), torch.cuda.Stream()]
+                outs = [out, torch.empty_like(out)]
+                torch.cuda.synchronize()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(s)
+                for st in ss:
+                    st.wait_event(a)
+                for k in range(args.stream_frames):
+                    r.render_rows_device(p, outs[k & 1].data_ptr(), T, rank, n, ss[k & 1].cuda_stream)
+                for st in ss:
+                    s.wait_stream(st)
+                b.record(s)
+                b.synchronize()
+                ms = [a.elapsed_time(b) / args.stream_frames]  # per frame, overlapped
             per_rank.append(min(ms))
         worst = max(per_rank)
         if n == 1:
