@@ -324,11 +324,13 @@ __device__ __forceinline__ float box_near(float4 lo, float4 hi, F3 ri, F3 oi, fl
 }
 
 // kMode: 0 general walk over the table in LDS, 1 general walk over the table in
-// global memory, 2 ordered BVH.
+// global memory, 2 ordered BVH, 3 ordered BVH over single-sphere primitives only
+// (no generic-primitive code: fewer registers).
 template <int kMode, bool kCountT>
 struct LaneTracer {
     static constexpr bool kCount = kCountT;
-    static constexpr bool kBvh = kMode == 2;
+    static constexpr bool kBvh = kMode >= 2;
+    static constexpr bool kSpheresOnly = kMode == 3;
     WorkCounts wk;
     uint64_t tmark;  // section timing (counting builds)
     const WoRec* __restrict__ prog;      // full program (generic primitives, hit leaves)
@@ -348,7 +350,7 @@ struct LaneTracer {
     // Interval of primitive `ord` (the general walk's arithmetic, bit for bit).
     __device__ __forceinline__ Ivl prim_ivl(uint32_t ord, F3 o, F3 d, F3& inv, bool& have_inv) {
         Ivl iv;
-        if (lkind[ord] != 0u) {
+        if (kSpheresOnly || lkind[ord] != 0u) {
             WO_WK(WO_WORK_SPHERE_TESTS);
             const float4 g = lgeo[ord];
             float b, ll, la, lb;
@@ -920,6 +922,7 @@ struct WoDev {
     float4* d_lbvh;
     size_t lbvh_cap;
     uint32_t lb_nodes, lb_always, lb_root, lb_nprims;
+    bool lb_spheres_only;  // every primitive is a single sphere (kMode 3)
     unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
     unsigned long long* d_work;      // WO_WORK_KINDS totals of a counting launch
     // progressive accumulation (3 int64 per pixel) and the draw_frame pipeline:
@@ -1275,6 +1278,7 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     dev->lb_nodes = dev->lb_always = 0;
     dev->lb_root = kNoRef;
     dev->lb_nprims = n_prims;
+    dev->lb_spheres_only = false;
     const char* env = getenv("WOLOLO_LANES_BVH");
     if (!dev->union_only || (env && env[0] == '0')) return 0;
     std::vector<LbPrim> prims;
@@ -1338,6 +1342,7 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     }
     dev->lb_nodes = (uint32_t)(nodes.size() / 4u);
     dev->lb_always = (uint32_t)always.size();
+    dev->lb_spheres_only = std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
     const size_t f4 = nodes.size() + n_prims;
     const size_t bytes = f4 * sizeof(float4) + ((size_t)n_prims + always.size()) * sizeof(uint32_t);
     if (ensure_buffer(&dev->d_lbvh, &dev->lbvh_cap, bytes, err, errlen)) return -1;
@@ -1691,7 +1696,7 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
     return wo_dev_launch_ex(dev, frame_in, d_out, stream_v, d_segments, nullptr, 0u, err, errlen);
 }
 
-enum PathKind { kLanesLds, kLanesGlobal, kLanesBvh, kJit, kInterpLds, kInterpGlobal };
+enum PathKind { kLanesLds, kLanesGlobal, kLanesBvh, kLanesBvhSpheres, kJit, kInterpLds, kInterpGlobal };
 
 template <bool kCount>
 static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
@@ -1702,6 +1707,8 @@ static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<1, kCount>, kBlock, dyn_lds);
     case kLanesBvh:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<2, kCount>, kBlock, dyn_lds);
+    case kLanesBvhSpheres:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<3, kCount>, kBlock, dyn_lds);
     case kInterpLds:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_kernel<true, kCount>, kBlock, dyn_lds);
     default:
@@ -1726,6 +1733,11 @@ static void static_launch(PathKind kind, dim3 grid, size_t dyn_lds, hipStream_t 
         break;
     case kLanesBvh:
         hipLaunchKernelGGL((pathtrace_lanes_kernel<2, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesBvhSpheres:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<3, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
                            dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
                            lane_bvh(dev));
         break;
@@ -1807,7 +1819,7 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
             // in LDS when it fits
             const size_t table = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
             if (dev->lb_root != kNoRef || dev->lb_always != 0u) {
-                kind = kLanesBvh;
+                kind = dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh;
                 dyn_lds = (size_t)kLaneStack * kBlock * sizeof(uint32_t);
             } else {
                 kind = table <= kLanesLdsBudget ? kLanesLds : kLanesGlobal;
