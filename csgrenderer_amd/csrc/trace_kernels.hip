@@ -344,6 +344,8 @@ struct LaneTracer {
     const uint32_t* __restrict__ lkind;  // per ordinal: 1 = single sphere, 0 = generic; then the always list
     uint32_t nalways, lroot, nprims;
     uint32_t* stk;                       // LDS stack column of this lane ([entry][lane])
+    const float4* ltop;                  // LDS copy of nodes [0, ntop) (the top levels, BFS order)
+    uint32_t ntop;
 
     __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const { return prog[ordpc[h.ord] + 1u + h.member]; }
 
@@ -419,8 +421,14 @@ struct LaneTracer {
                 cur = kNoRef;
             } else {
                 WO_WK_N(WO_WORK_BOUND_TESTS, 2u);
-                const float4* nd = lnodes + 4u * cur;
-                const float4 a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                float4 a0, a1, b0, b1;
+                if (cur < ntop) {  // the top levels: LDS latency instead of a cache round trip
+                    const float4* nd = ltop + 4u * cur;
+                    a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                } else {
+                    const float4* nd = lnodes + 4u * cur;
+                    a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                }
                 // useful range: up to the best event so far
                 const float tb = best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(best >> 32));
                 float fa, fb;
@@ -617,6 +625,7 @@ struct LaneBvh {
     const float4* geo;
     const uint32_t* kind;  // per ordinal, then the always list
     uint32_t nalways, root, nprims;
+    uint32_t ntop;         // nodes [0, ntop) staged in LDS after the lane stacks
 };
 
 // Dynamic LDS: the lane stacks ([kLaneStack][kBlock] u32), then (kLds) the
@@ -641,7 +650,17 @@ __global__ __launch_bounds__(kBlock, kMode == 2 ? WO_LANES_BVH_MIN_WAVES : WO_LA
     tr.nalways = bvh.nalways;
     tr.lroot = bvh.root;
     tr.nprims = bvh.nprims;
-    tr.stk = smem + threadIdx.x;  // kMode 2 only
+    tr.stk = smem + threadIdx.x;  // kMode >= 2 only
+    tr.ntop = 0;
+    tr.ltop = nullptr;
+    if constexpr (kMode >= 2) {
+        // the top levels of the BVH next to the stacks; pathtrace_block's first
+        // barrier orders the copy before any walk
+        float4* top = reinterpret_cast<float4*>(smem + kLaneStack * kBlock);
+        for (uint32_t i = threadIdx.x; i < 4u * bvh.ntop; i += kBlock) top[i] = bvh.nodes[i];
+        tr.ltop = top;
+        tr.ntop = bvh.ntop;
+    }
     const uint32_t* gaux = reinterpret_cast<const uint32_t*>(gnodes + ntrav);
     if constexpr (kLds) {
         uint32_t* table = smem;
@@ -923,6 +942,7 @@ struct WoDev {
     size_t lbvh_cap;
     uint32_t lb_nodes, lb_always, lb_root, lb_nprims;
     bool lb_spheres_only;  // every primitive is a single sphere (kMode 3)
+    uint32_t lb_top;       // nodes staged in LDS per workgroup
     unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
     unsigned long long* d_work;      // WO_WORK_KINDS totals of a counting launch
     // progressive accumulation (3 int64 per pixel) and the draw_frame pipeline:
@@ -1275,7 +1295,7 @@ static uint32_t lb_build(std::vector<LbPrim>& prims, uint32_t b, uint32_t e, std
 // ground sphere, which every ray meets anyway).  WOLOLO_LANES_BVH=0: none (the
 // general walk only).
 static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n_prims, char* err, size_t errlen) {
-    dev->lb_nodes = dev->lb_always = 0;
+    dev->lb_nodes = dev->lb_always = dev->lb_top = 0;
     dev->lb_root = kNoRef;
     dev->lb_nprims = n_prims;
     dev->lb_spheres_only = false;
@@ -1339,9 +1359,46 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     if (!prims.empty()) {
         LbBox root_box;
         dev->lb_root = lb_build(prims, 0u, (uint32_t)prims.size(), nodes, root_box);
+        // breadth-first node order: the top levels are then nodes [0, k), the ones
+        // every walk visits first, and they are staged in LDS (lb_top)
+        if (!(dev->lb_root & kLeafRef)) {
+            const uint32_t nn = (uint32_t)(nodes.size() / 4u);
+            auto ref_at = [&](uint32_t n, int c) {
+                uint32_t u;
+                memcpy(&u, &nodes[4u * n + (uint32_t)c].w, sizeof u);
+                return u;
+            };
+            std::vector<uint32_t> order, newidx(nn, 0u);
+            order.reserve(nn);
+            order.push_back(dev->lb_root);
+            for (size_t h = 0; h < order.size(); ++h)
+                for (int c = 0; c < 2; ++c) {
+                    const uint32_t r = ref_at(order[h], c);
+                    if (!(r & kLeafRef)) order.push_back(r);
+                }
+            for (uint32_t i = 0; i < nn; ++i) newidx[order[i]] = i;
+            std::vector<float4> bfs(nodes.size());
+            for (uint32_t i = 0; i < nn; ++i) {
+                for (int k = 0; k < 4; ++k) bfs[4u * i + (uint32_t)k] = nodes[4u * order[i] + (uint32_t)k];
+                for (int c = 0; c < 2; ++c) {
+                    uint32_t r = ref_at(order[i], c);
+                    if (!(r & kLeafRef)) r = newidx[r];
+                    memcpy(&bfs[4u * i + (uint32_t)c].w, &r, sizeof r);
+                }
+            }
+            nodes.swap(bfs);
+            dev->lb_root = 0u;
+        }
     }
     dev->lb_nodes = (uint32_t)(nodes.size() / 4u);
     dev->lb_always = (uint32_t)always.size();
+    {
+        // 32 nodes (2 KB) keep 8 workgroups per CU within the 160 KB of LDS
+        uint32_t top = 32u;
+        const char* v = getenv("WOLOLO_LANES_TOP");
+        if (v && *v) top = (uint32_t)strtoul(v, NULL, 10);
+        dev->lb_top = top < dev->lb_nodes ? top : dev->lb_nodes;
+    }
     dev->lb_spheres_only = std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
     const size_t f4 = nodes.size() + n_prims;
     const size_t bytes = f4 * sizeof(float4) + ((size_t)n_prims + always.size()) * sizeof(uint32_t);
@@ -1368,6 +1425,7 @@ static LaneBvh lane_bvh(const WoDev* dev) {
     b.nalways = dev->lb_always;
     b.root = dev->lb_root;
     b.nprims = dev->lb_nprims;
+    b.ntop = dev->lb_top;
     return b;
 }
 
@@ -1820,7 +1878,7 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
             const size_t table = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
             if (dev->lb_root != kNoRef || dev->lb_always != 0u) {
                 kind = dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh;
-                dyn_lds = (size_t)kLaneStack * kBlock * sizeof(uint32_t);
+                dyn_lds = (size_t)kLaneStack * kBlock * sizeof(uint32_t) + (size_t)dev->lb_top * 4u * sizeof(float4);
             } else {
                 kind = table <= kLanesLdsBudget ? kLanesLds : kLanesGlobal;
                 dyn_lds = kind == kLanesLds ? table : 0u;
