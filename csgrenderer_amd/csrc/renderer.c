@@ -510,6 +510,11 @@ int wo_renderer_jit_info(Wo_Renderer* r, double* seconds) {
     return wo_dev_jit_origin(r->dev, seconds);
 }
 
+int wo_renderer_lanes_info(Wo_Renderer* r, uint32_t* out) {
+    if (!r || !r->dev || !r->lanes_loaded || !out) return -1;
+    return wo_dev_lanes_info(r->dev, out);
+}
+
 char const* wo_renderer_trace_path(Wo_Renderer* r) {
     if (!r->dev) return "none";
     return r->jit_loaded ? "jit" : r->lanes_loaded ? "lanes" : "interpreter";

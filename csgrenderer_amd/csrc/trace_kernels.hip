@@ -309,7 +309,13 @@ constexpr uint32_t kNodeBound = 0u, kNodeSphere = 1u, kNodeGeneric = 2u;
 // bit.  A ray that starts inside some primitive (counted on the way: boxes that
 // contain the ray's start are never pruned) takes the general walk below.
 constexpr uint32_t kLeafRef = 0x80000000u, kNoRef = 0xffffffffu;
-constexpr uint32_t kLaneStack = 16;  // per-lane LDS stack entries (power of 2)
+// The lane BVH is built with at most kLaneDepthMax internal levels on any path,
+// and the per-lane LDS stack holds as many entries as the built tree has levels:
+// a walk pushes at most one sibling per ancestor, so the stack never overflows.
+constexpr uint32_t kLaneDepthMax = 24;
+// dynamic LDS of the BVH walk (stacks + top nodes): with the kernel's static LDS,
+// 8 workgroups of kBlock fit in a CU's 160 KB
+constexpr size_t kLanesBvhLds = 18u * 1024u;
 
 // Slab test of a ray against an expanded AABB: [near, far] of the ray's overlap
 // (conservative: the boxes carry the slack; `ri` = reciprocal direction with
@@ -413,8 +419,7 @@ struct LaneTracer {
         };
         uint32_t in_always = 0, in_tree = 0;
         for (uint32_t i = 0; i < nalways; ++i) visit(lkind[nprims + i], in_always);
-        uint32_t cur = lroot, sp = 0, bottom = 0;
-        bool lost = false;
+        uint32_t cur = lroot, sp = 0;
         while (cur != kNoRef) {
             if (cur & kLeafRef) {
                 visit(cur & ~kLeafRef, in_tree);
@@ -440,26 +445,15 @@ struct LaneTracer {
                     const bool a_first = na <= nb;
                     cur = a_first ? ra : rb;
                     const uint32_t other = a_first ? rb : ra;
-                    if (sp - bottom == kLaneStack) {  // full: drop the oldest, walk again later
-                        ++bottom;
-                        lost = true;
-                    }
-                    stk[(sp & (kLaneStack - 1u)) * kBlock] = other;
+                    stk[sp * kBlock] = other;  // sp < the tree's depth (build_lbvh)
                     ++sp;
                 } else {
                     cur = ha ? ra : (hb ? rb : kNoRef);
                 }
             }
-            if (cur == kNoRef) {
-                if (sp != bottom) {
-                    --sp;
-                    cur = stk[(sp & (kLaneStack - 1u)) * kBlock];
-                } else if (lost) {  // entries were dropped: walk again (the minimum is idempotent)
-                    lost = false;
-                    sp = bottom = 0;
-                    in_tree = 0;
-                    cur = lroot;
-                }
+            if (cur == kNoRef && sp != 0u) {
+                --sp;
+                cur = stk[sp * kBlock];
             }
         }
         inside = in_always + in_tree;
@@ -625,11 +619,12 @@ struct LaneBvh {
     const float4* geo;
     const uint32_t* kind;  // per ordinal, then the always list
     uint32_t nalways, root, nprims;
+    uint32_t depth;        // internal levels of the tree: the lane stack's entries
     uint32_t ntop;         // nodes [0, ntop) staged in LDS after the lane stacks
 };
 
-// Dynamic LDS: the lane stacks ([kLaneStack][kBlock] u32), then (kLds) the
-// general walk's table.
+// Dynamic LDS: the BVH walk's lane stacks ([depth][kBlock] u32) and top nodes,
+// or (kLds) the general walk's table.
 #ifndef WO_LANES_BVH_MIN_WAVES
 #define WO_LANES_BVH_MIN_WAVES 7  // rtiow_cover: 16.86 ms at 8, 16.63 at 7, 17.26 at 6
 #endif
@@ -656,7 +651,7 @@ __global__ __launch_bounds__(kBlock, kMode == 2 ? WO_LANES_BVH_MIN_WAVES : WO_LA
     if constexpr (kMode >= 2) {
         // the top levels of the BVH next to the stacks; pathtrace_block's first
         // barrier orders the copy before any walk
-        float4* top = reinterpret_cast<float4*>(smem + kLaneStack * kBlock);
+        float4* top = reinterpret_cast<float4*>(smem + bvh.depth * kBlock);
         for (uint32_t i = threadIdx.x; i < 4u * bvh.ntop; i += kBlock) top[i] = bvh.nodes[i];
         tr.ltop = top;
         tr.ntop = bvh.ntop;
@@ -943,6 +938,7 @@ struct WoDev {
     uint32_t lb_nodes, lb_always, lb_root, lb_nprims;
     bool lb_spheres_only;  // every primitive is a single sphere (kMode 3)
     uint32_t lb_top;       // nodes staged in LDS per workgroup
+    uint32_t lb_depth;     // internal levels of the lane BVH (<= kLaneDepthMax)
     unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
     unsigned long long* d_work;      // WO_WORK_KINDS totals of a counting launch
     // progressive accumulation (3 int64 per pixel) and the draw_frame pipeline:
@@ -1214,13 +1210,23 @@ struct LbBox {
     }
 };
 
-// Binned-SAH build over prims[b, e); returns the subtree's ref.  Node n is
-// written to nodes[4n..4n+3] as the two children's boxes (rounded outward to
-// float) with their refs in the .w of the first two.
-static uint32_t lb_build(std::vector<LbPrim>& prims, uint32_t b, uint32_t e, std::vector<float4>& nodes,
-                         LbBox& box_out) {
+static uint32_t ceil_log2(uint32_t c) {
+    uint32_t k = 0;
+    while ((1ull << k) < c) ++k;
+    return k;
+}
+
+// Binned-SAH build over prims[b, e) with at most `levels` internal levels below
+// (ceil_log2(e - b) <= levels on entry); returns the subtree's ref and its
+// depth.  A SAH split that would leave a child more primitives than its levels
+// can hold becomes the median split, which always fits.  Node n is written to
+// nodes[4n..4n+3] as the two children's boxes (rounded outward to float) with
+// their refs in the .w of the first two.
+static uint32_t lb_build(std::vector<LbPrim>& prims, uint32_t b, uint32_t e, uint32_t levels,
+                         std::vector<float4>& nodes, LbBox& box_out, uint32_t& depth_out) {
     box_out.empty();
     for (uint32_t i = b; i < e; ++i) box_out.grow(prims[i].lo, prims[i].hi);
+    depth_out = 0;
     if (e - b == 1u) return kLeafRef | prims[b].ord;
     LbBox cb;
     cb.empty();
@@ -1263,7 +1269,8 @@ static uint32_t lb_build(std::vector<LbPrim>& prims, uint32_t b, uint32_t e, std
             mid = (uint32_t)(it - prims.begin());
         }
     }
-    if (mid == b || mid == e) {  // no useful split: the median along the axis
+    if (mid == b || mid == e || ceil_log2(mid - b) >= levels || ceil_log2(e - mid) >= levels) {
+        // no useful split, or one too deep for the lane stack: the median along the axis
         mid = b + (e - b) / 2u;
         std::nth_element(prims.begin() + b, prims.begin() + mid, prims.begin() + e,
                          [&](const LbPrim& x, const LbPrim& y) { return x.c[axis] < y.c[axis]; });
@@ -1271,8 +1278,10 @@ static uint32_t lb_build(std::vector<LbPrim>& prims, uint32_t b, uint32_t e, std
     const uint32_t n = (uint32_t)(nodes.size() / 4u);
     nodes.resize(nodes.size() + 4u);
     LbBox lb, rb;
-    const uint32_t lref = lb_build(prims, b, mid, nodes, lb);
-    const uint32_t rref = lb_build(prims, mid, e, nodes, rb);
+    uint32_t ld, rd;
+    const uint32_t lref = lb_build(prims, b, mid, levels - 1u, nodes, lb, ld);
+    const uint32_t rref = lb_build(prims, mid, e, levels - 1u, nodes, rb, rd);
+    depth_out = 1u + (ld > rd ? ld : rd);
     auto bits_f = [](uint32_t u) {
         float f;
         memcpy(&f, &u, sizeof f);
@@ -1295,7 +1304,7 @@ static uint32_t lb_build(std::vector<LbPrim>& prims, uint32_t b, uint32_t e, std
 // ground sphere, which every ray meets anyway).  WOLOLO_LANES_BVH=0: none (the
 // general walk only).
 static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n_prims, char* err, size_t errlen) {
-    dev->lb_nodes = dev->lb_always = dev->lb_top = 0;
+    dev->lb_nodes = dev->lb_always = dev->lb_top = dev->lb_depth = 0;
     dev->lb_root = kNoRef;
     dev->lb_nprims = n_prims;
     dev->lb_spheres_only = false;
@@ -1356,9 +1365,16 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
         prims.swap(kept);
     }
     std::vector<float4> nodes;
+    if (ceil_log2((uint32_t)prims.size()) > kLaneDepthMax) return 0;  // > 2^24 primitives: the general walk
     if (!prims.empty()) {
+        // levels: SAH's freedom over the balanced tree's log2(n), within the stack's limit
+        uint32_t levels = ceil_log2((uint32_t)prims.size()) + 6u;
+        const char* lv = getenv("WOLOLO_LANES_DEPTH");
+        if (lv && *lv) levels = (uint32_t)strtoul(lv, NULL, 10);
+        if (levels < ceil_log2((uint32_t)prims.size())) levels = ceil_log2((uint32_t)prims.size());
+        if (levels > kLaneDepthMax) levels = kLaneDepthMax;
         LbBox root_box;
-        dev->lb_root = lb_build(prims, 0u, (uint32_t)prims.size(), nodes, root_box);
+        dev->lb_root = lb_build(prims, 0u, (uint32_t)prims.size(), levels, nodes, root_box, dev->lb_depth);
         // breadth-first node order: the top levels are then nodes [0, k), the ones
         // every walk visits first, and they are staged in LDS (lb_top)
         if (!(dev->lb_root & kLeafRef)) {
@@ -1393,8 +1409,9 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     dev->lb_nodes = (uint32_t)(nodes.size() / 4u);
     dev->lb_always = (uint32_t)always.size();
     {
-        // 32 nodes (2 KB) keep 8 workgroups per CU within the 160 KB of LDS
-        uint32_t top = 32u;
+        // the top nodes fill what the stacks leave of kLanesBvhLds (8 workgroups per CU)
+        const size_t stacks = (size_t)dev->lb_depth * kBlock * sizeof(uint32_t);
+        uint32_t top = stacks < kLanesBvhLds ? (uint32_t)((kLanesBvhLds - stacks) / (4u * sizeof(float4))) : 0u;
         const char* v = getenv("WOLOLO_LANES_TOP");
         if (v && *v) top = (uint32_t)strtoul(v, NULL, 10);
         dev->lb_top = top < dev->lb_nodes ? top : dev->lb_nodes;
@@ -1426,6 +1443,7 @@ static LaneBvh lane_bvh(const WoDev* dev) {
     b.root = dev->lb_root;
     b.nprims = dev->lb_nprims;
     b.ntop = dev->lb_top;
+    b.depth = dev->lb_depth;
     return b;
 }
 
@@ -1668,6 +1686,15 @@ extern "C" int wo_dev_jit_origin(WoDev* dev, double* seconds) {
     return dev->jit_origin;
 }
 
+extern "C" int wo_dev_lanes_info(WoDev* dev, uint32_t* out) {
+    if (!dev) return -1;
+    out[0] = dev->lb_nodes;
+    out[1] = dev->lb_depth;
+    out[2] = dev->lb_top;
+    out[3] = dev->lb_always;
+    return 0;
+}
+
 extern "C" int wo_jit_compile_check(const char* src, const char* arch, char* err, size_t errlen) {
     std::vector<char> code;
     return jit_compile(src, arch ? std::string(arch) : std::string("gfx950"), false, code, err, errlen);
@@ -1878,7 +1905,7 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
             const size_t table = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
             if (dev->lb_root != kNoRef || dev->lb_always != 0u) {
                 kind = dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh;
-                dyn_lds = (size_t)kLaneStack * kBlock * sizeof(uint32_t) + (size_t)dev->lb_top * 4u * sizeof(float4);
+                dyn_lds = (size_t)dev->lb_depth * kBlock * sizeof(uint32_t) + (size_t)dev->lb_top * 4u * sizeof(float4);
             } else {
                 kind = table <= kLanesLdsBudget ? kLanesLds : kLanesGlobal;
                 dyn_lds = kind == kLanesLds ? table : 0u;

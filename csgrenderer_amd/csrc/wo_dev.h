@@ -92,6 +92,7 @@ int wo_jit_disk_store(const char* key_hex, const void* code, size_t size);
 /* Origin (as above; -1: no specialised kernel) and seconds of the object the
  * device's specialised kernel was loaded from. */
 int wo_dev_jit_origin(WoDev* dev, double* seconds);
+int wo_dev_lanes_info(WoDev* dev, uint32_t* out);
 /* Wait for the slot's frame; *host = its pixels (RGBA float), *host_bgra8 (if
  * non-NULL) = its present encode; both valid until the slot is submitted again. */
 int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, uint32_t const** host_bgra8, char* err,

@@ -136,6 +136,7 @@ SIGNATURES = {
     "wo_jit_code_object": (ctypes.c_longlong, [c_char_p, c_char_p, POINTER(c_int), POINTER(c_double), c_char_p,
                                                c_char_p, c_size_t]),
     "wo_renderer_jit_info": (c_int, [c_void_p, POINTER(c_double)]),
+    "wo_renderer_lanes_info": (c_int, [c_void_p, POINTER(c_uint32)]),
     "wo_free": (None, [c_void_p]),
     "wo_renderer_node_count": (c_size_t, [c_void_p]),
     "wo_renderer_name": (c_char_p, [c_void_p]),
@@ -297,6 +298,13 @@ class Renderer:
         sec = c_double(0.0)
         o = self.lib.wo_renderer_jit_info(self.ptr, ctypes.byref(sec))
         return (None if o < 0 else JIT_ORIGINS[o]), sec.value
+
+    def lanes_info(self):
+        """The lane tracer's BVH: {"nodes", "depth", "top", "always"}, or None if not on the lane tracer."""
+        out = (c_uint32 * 4)()
+        if self.lib.wo_renderer_lanes_info(self.ptr, out) < 0:
+            return None
+        return dict(zip(("nodes", "depth", "top", "always"), list(out)))
 
     def set_jit(self, mode: int):
         self.lib.wo_renderer_set_jit(self.ptr, int(mode))

@@ -198,6 +198,11 @@ long long wo_jit_code_object(char const* src, char const* arch, int* origin, dou
 /* Where the renderer's specialised kernel came from (origin as above; -1: the
  * renderer does not run one) and the seconds it took (compile or load). */
 int wo_renderer_jit_info(Wo_Renderer* r, double* seconds);
+/* The lane tracer's BVH (union-only scenes): out[0] internal nodes, out[1] its
+ * depth in internal levels (= the per-lane LDS stack entries; at most 24),
+ * out[2] top nodes staged in LDS, out[3] primitives tested on every query (no
+ * box).  Returns 0, or -1 when the renderer does not run the lane tracer. */
+int wo_renderer_lanes_info(Wo_Renderer* r, uint32_t* out);
 void wo_free(void* p);
 
 size_t wo_renderer_node_count(Wo_Renderer* r);

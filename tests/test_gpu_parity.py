@@ -391,6 +391,42 @@ def test_lanes_union_scene_bitexact(tracer, monkeypatch):
     r.close()
 
 
+@pytest.mark.parametrize("levels", [None, "0"])
+def test_lanes_bvh_depth_bound(levels, monkeypatch):
+    """A chain of spheres at exponentially growing spacing: binned SAH splits off one
+    far sphere at a time, a tree as deep as the scene is long without the depth
+    bound.  build_lbvh bounds the depth (log2(n) + 6 levels by default; a request below
+    log2(n), here 0, gives the balanced tree) so the per-lane LDS stack, sized by the
+    depth, never overflows, and the image stays the oracle's."""
+    if levels is not None:
+        monkeypatch.setenv("WOLOLO_LANES_DEPTH", levels)
+    monkeypatch.setenv("WOLOLO_LANES_MIN_PRIMS", "64")
+    r = wl.Renderer("deep", max_nodes=4096)
+    n = 600
+    items = []
+    for i in range(n):
+        s = r.sphere(0.05 + 0.02 * (i % 3))
+        x = 0.1 * (1.02 ** i - 1.0)
+        items.append(wl.arg(s, (x - 3.0, 0.3 * np.sin(i), -0.2 * (i % 5))))
+    while len(items) > 1:
+        nxt = [wl.arg(r.union(items[i], items[i + 1])) for i in range(0, len(items) - 1, 2)]
+        if len(items) % 2:
+            nxt.append(items[-1])
+        items = nxt
+    r.set_camera((-3.5, 0.5, 3.0), (0.0, 0.0, -1.0), (0, 1, 0), 60.0)
+    r.set_tracer("lanes")
+    p = wl.render_params(64, 40, spp=2, max_depth=6, mode=wl.MODE_PATHTRACE, seed=7)
+    img = r.render(p)
+    assert r.trace_path() == "lanes"
+    info = r.lanes_info()
+    log2n = int(np.ceil(np.log2(n)))
+    assert info["depth"] <= (log2n if levels == "0" else log2n + 6), info
+    assert info["nodes"] == n - info["always"] - 1  # a binary tree over the boxed primitives
+    ref, _ = _oracle_rows(r, p)
+    _cmp(img, ref, f"deep chain, levels={levels}")
+    r.close()
+
+
 def test_auto_tracer_choices():
     """AUTO: the RTIOW cover (union-only, 487 primitives) takes the lane tracer; csg32 and a
     128-primitive union-only scene the JIT."""
