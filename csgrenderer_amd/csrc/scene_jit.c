@@ -770,7 +770,12 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "  tr.ordpc = kOrdPc;\n"
          "  const WoMaterial* m = mats;\n"
          "#endif\n"
+         "#if WO_JIT_LDS_EVENTS && WO_SORT_RAYS\n"
+         "  static_assert(wodev::kLdsEvents >= 6u, \"a ray's state fits the event list column\");\n"
+         "  wodev::pathtrace_block<JitTracer, true>(tr, m, fr, local_rows, out, seg_slots, tg, s_ev);\n"
+         "#else\n"
          "  wodev::pathtrace_block(tr, m, fr, local_rows, out, seg_slots, tg);\n"
+         "#endif\n"
          "}\n",
          n_recs ? n_recs : 1u, n_mats_used, n_prims ? n_prims : 1u, n_recs * 8u, n_mats_used * 8u, n_prims);
     if (g.err || b.oom) {
