@@ -350,7 +350,17 @@ struct LaneTracer {
     const uint32_t* __restrict__ lkind;  // per ordinal: 1 = single sphere, 0 = generic; then the always list
     uint32_t nalways, lroot, nprims;
     uint32_t* stk;                       // LDS stack column of this lane ([entry][lane])
-    const float4* ltop;                  // LDS copy of nodes [0, ntop) (the top levels, BFS order)
+    // LDS copy of nodes [0, ntop) (the top levels, BFS order).  Typed by address
+    // space so the two node reads of query() stay an LDS and a global load: one
+    // pointer to either would be a flat load, which waits on both counters.
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(3))) float4* LdsNodes;
+    typedef const __attribute__((address_space(1))) float4* GlobalNodes;
+#else
+    typedef const float4* LdsNodes;
+    typedef const float4* GlobalNodes;
+#endif
+    LdsNodes ltop;
     uint32_t ntop;
 
     __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const { return prog[ordpc[h.ord] + 1u + h.member]; }
@@ -428,10 +438,11 @@ struct LaneTracer {
                 WO_WK_N(WO_WORK_BOUND_TESTS, 2u);
                 float4 a0, a1, b0, b1;
                 if (cur < ntop) {  // the top levels: LDS latency instead of a cache round trip
-                    const float4* nd = ltop + 4u * cur;
+                    const LdsNodes nd = ltop + 4u * cur;
                     a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                    asm volatile("");  // the branches' tails differ: the loads are not merged into flat loads
                 } else {
-                    const float4* nd = lnodes + 4u * cur;
+                    const GlobalNodes nd = (GlobalNodes)lnodes + 4u * cur;
                     a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
                 }
                 // useful range: up to the best event so far
@@ -647,13 +658,13 @@ __global__ __launch_bounds__(kBlock, kMode == 2 ? WO_LANES_BVH_MIN_WAVES : WO_LA
     tr.nprims = bvh.nprims;
     tr.stk = smem + threadIdx.x;  // kMode >= 2 only
     tr.ntop = 0;
-    tr.ltop = nullptr;
+    tr.ltop = (typename LaneTracer<kMode, kCount>::LdsNodes)nullptr;
     if constexpr (kMode >= 2) {
         // the top levels of the BVH next to the stacks; pathtrace_block's first
         // barrier orders the copy before any walk
         float4* top = reinterpret_cast<float4*>(smem + bvh.depth * kBlock);
         for (uint32_t i = threadIdx.x; i < 4u * bvh.ntop; i += kBlock) top[i] = bvh.nodes[i];
-        tr.ltop = top;
+        tr.ltop = (typename LaneTracer<kMode, kCount>::LdsNodes)top;
         tr.ntop = bvh.ntop;
     }
     const uint32_t* gaux = reinterpret_cast<const uint32_t*>(gnodes + ntrav);
