@@ -93,6 +93,7 @@ typedef struct Gen {
     int pair_window;  /* LDS event list behind two register slots (PairLdsWindow) */
     int lit_consts;   /* sphere / BOUND / axis-face constants as VALU literal operands instead of scalar moves */
     int first_event;  /* the first event of waves that start outside every primitive from a constant table */
+    int fused_sphere; /* a lone sphere's membership and events inside its sqrt branch (no empty interval) */
     int err;
 } Gen;
 
@@ -109,6 +110,8 @@ static int bound_tested(const Gen* g, uint32_t pc) {
 }
 
 /* ---- collect: intersect every primitive of [start, end), fill the window ---- */
+static void gen_lone_sphere(Gen* g, const WoRec* L, uint32_t ord, int indent);
+
 static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
     uint32_t pc = start;
     while (pc < end && !g->err) {
@@ -156,6 +159,11 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
             static const char* nl[4] = {"c0", "c1", "c2", "c3"};
             static const char* nk[2] = {"ka", "kb"};
             bput(g->b, "%*s{  // primitive %u (%u leaves)\n", indent, "", ord, cnt);
+            if (cnt == 1u && g->fused_sphere && g->lit_consts && g->prog[pc + 1].op == WO_LEAF_SPHERE) {
+                gen_lone_sphere(g, &g->prog[pc + 1], ord, indent);
+                pc += 2;
+                continue;
+            }
             bput(g->b, "%*s  wodev::Ivl iv; float la, lb;\n", indent, "");
             int open_skips = 0;
             for (uint32_t m = 0; m < cnt; ++m) {
@@ -266,6 +274,45 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
             ++pc; /* binops: nothing to collect */
         }
     }
+}
+
+/* A primitive that is one sphere: its interval is [-b - s, -b + s] exactly when
+ * disc >= 0, so the membership bit and the events are set inside the branch that
+ * computes s (the lanes that skip it have an empty interval, as in
+ * sphere_interval_bd: same bits and events) and no empty interval is formed.
+ * Member index 0 (ivl_first). */
+static void gen_lone_sphere(Gen* g, const WoRec* L, uint32_t ord, int indent) {
+    uint32_t vl[4];
+    for (int i = 0; i < 4; ++i) vl[i] = fbits(L->f[i]);
+    bput(g->b,
+         "%*s  WO_WK(WO_WORK_SPHERE_TESTS);\n"
+         "%*s  float fx, fy, fz, b, ll, disc;\n"
+         "%*s  asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fx) : \"v\"(o.x));\n"
+         "%*s  asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fy) : \"v\"(o.y));\n"
+         "%*s  asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fz) : \"v\"(o.z));\n"
+         "%*s  wodev::sphere_fbl(fx, fy, fz, d, b, ll);\n"
+         "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(disc) : \"v\"(ll));\n"
+         "%*s  if (__ballot(wodev::sphere_need(b, disc)) != 0ull) {\n"
+         "%*s    asm volatile(\"\");\n"
+         "%*s    if (!(disc < 0.0f)) {\n"
+         "%*s      const float s = wodev::sqrt_pt(disc), nb = -b, la = nb - s, lb = nb + s;\n"
+         "%*s      uint32_t ka, kb;\n"
+         "%*s      asm volatile(\"s_mov_b32 %%0, 0x%08x\\n\\ts_mov_b32 %%1, 0x%08x\" : \"=s\"(ka), \"=s\"(kb));\n",
+         indent, "", indent, "", indent, "", vl[0], indent, "", vl[1], indent, "", vl[2], indent, "", indent, "", vl[3],
+         indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", ord << 12, (ord << 12) | (1u << 11));
+    if (g->first_pass)
+        bput(g->b,
+             "%*s      bits[%u] |= ((la <= tmin && lb > tmin) ? 1u : 0u) << %u;\n"
+             "%*s      if (la > tmin) { WO_WK(WO_WORK_EVENTS); win.insert(wodev::event_key_lo(la, ka)); }\n"
+             "%*s      if ((lb > tmin) & (lb < wodev::kInf)) { WO_WK(WO_WORK_EVENTS); win.insert(wodev::event_key_lo(lb, kb)); }\n",
+             indent, "", ord / 32, ord % 32, indent, "", indent, "");
+    else
+        bput(g->b,
+             "%*s      const uint64_t k0 = wodev::event_key_lo(la, ka), k1 = wodev::event_key_lo(lb, kb);\n"
+             "%*s      if ((la > tmin) & (k0 > after)) { WO_WK(WO_WORK_EVENTS); win.insert(k0); }\n"
+             "%*s      if ((lb > tmin) & (lb < wodev::kInf) & (k1 > after)) { WO_WK(WO_WORK_EVENTS); win.insert(k1); }\n",
+             indent, "", indent, "", indent, "");
+    bput(g->b, "%*s    }\n%*s  }\n%*s}\n", indent, "", indent, "", indent, "");
 }
 
 /* ---- eval: value of the subtree [start, end) as named 0/1 temporaries ---- */
@@ -557,6 +604,11 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     {
         const char* v = getenv("WOLOLO_JIT_LIT_CONSTS");
         if (v && *v) g.lit_consts = v[0] != '0';
+    }
+    g.fused_sphere = 1;
+    {
+        const char* v = getenv("WOLOLO_JIT_FUSED_SPHERE");
+        if (v && *v) g.fused_sphere = v[0] != '0';
     }
     g.first_event = n_prims <= 64u * 32u;
     {

@@ -19,8 +19,9 @@ def test_csg32_source_compiles_for_gfx950(hostonly):
     # each of the two collect passes (first pass, re-collect), one cull flag per
     # BOUND, ordinal table of every primitive
     nleaf = sum(1 for i in range(nrec) if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE))
-    # (a sphere with literal constants ends in sphere_interval_bd, an axis face in halfspace_axis_dist)
-    nsingle = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
+    # (a sphere with literal constants ends in sphere_interval_bd, or is a lone sphere tested with
+    # sphere_need; an axis face ends in halfspace_axis_dist)
+    nsingle = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|sphere_need|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
     npair = len(re.findall(r"wodev::axis_pair_meet(_d)?\(", src))
     assert npair >= 2 * 6  # the slab and the cube: three face pairs each, in both passes
     assert nsingle + 2 * npair == 2 * nleaf
@@ -82,7 +83,7 @@ def test_member_skip_guards(hostonly, monkeypatch):
     prog, nrec, _ = r.program()
     src = r.jit_source()
     pair_members = len(re.findall(r"wodev::axis_pair_meet(_d)?\(", src))  # a pair is one member step
-    singles = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
+    singles = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|sphere_need|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
     nprims_emitted = 2 * sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_PRIM)
     assert src.count(guard) == singles + pair_members - nprims_emitted > 0
     monkeypatch.setenv("WOLOLO_JIT_MEMBER_SKIP", "0")
