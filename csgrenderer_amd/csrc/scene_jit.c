@@ -733,6 +733,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  ") != 0u) == 0ull) {\n"
                  "      win.next(key);\n"
                  "      WO_WK(WO_WORK_SWEEP_STEPS);\n"
+                 "      WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);\n"
                  "      const uint32_t ord = ((uint32_t)key) >> 12;\n"
                  "      const uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n"
                  "      uint32_t single = 0u;\n");
@@ -776,6 +777,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "      }\n"
              "      have = true;\n"
              "      WO_WK(WO_WORK_SWEEP_STEPS);\n"
+                 "      WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);\n"
              "      {\n"
              "        uint32_t ord = ((uint32_t)key) >> 12;\n"
              "        uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n");

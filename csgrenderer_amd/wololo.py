@@ -29,7 +29,8 @@ TRACERS = {"auto": TRACER_AUTO, "interpreter": TRACER_INTERPRETER, "jit": TRACER
 WO_T_MIN = 1.0e-3
 # wo_scene.h WO_WORK_* (executed-work counters)
 WORK_KINDS = ("segments", "sphere_tests", "halfspace_tests", "bound_tests", "events", "sweep_steps", "recollects",
-              "primary_segments", "cyc_take", "cyc_collect", "cyc_sweep", "cyc_shade", "cyc_loop")
+              "primary_segments", "cyc_take", "cyc_collect", "cyc_sweep", "cyc_shade", "cyc_loop", "idle_lanes",
+              "sweep_trips")
 WO_NODE_INVALID = 0xFFFFFFFF
 
 

@@ -134,7 +134,10 @@ enum {
     WO_WORK_CYC_SWEEP = 10,      /* trace: sweep + re-collects */
     WO_WORK_CYC_SHADE = 11,      /* hit shading, scatter, accumulation */
     WO_WORK_CYC_LOOP = 12,       /* whole loop iterations */
-    WO_WORK_KINDS = 13
+    /* lane occupancy (counting launches): */
+    WO_WORK_IDLE_LANES = 13,     /* loop iterations of a lane with no path (queue drained) */
+    WO_WORK_SWEEP_TRIPS = 14,    /* sweep loop trips of a wave (64 lane slots each) */
+    WO_WORK_KINDS = 15
 };
 
 /* Minimum ray parameter for every CSG segment (RTIOW's 0.001). */

@@ -40,7 +40,11 @@ def main():
         out = {"scene": name, "path": r.trace_path(), "segments": segs,
                "per_segment": {k: round(w[k] / segs, 4) for k in wl.WORK_KINDS[1:8]},
                "cycle_share": {k: round(v / loop, 4) for k, v in cyc.items() if k != "cyc_loop"},
-               "wave_cycles_per_segment": round(loop / segs, 2)}
+               "wave_cycles_per_segment": round(loop / segs, 2),
+               # lane iterations without a path (the tile's queue drained), and the
+               # sweep loop's lane use (lane steps over 64 x wave trips)
+               "idle_lane_iterations": round(w["idle_lanes"] / max(segs + w["idle_lanes"], 1), 4),
+               "sweep_lane_use": round(w["sweep_steps"] / max(64 * w["sweep_trips"], 1), 4)}
         print(json.dumps(out), flush=True)
         r.close()
 
