@@ -1745,8 +1745,14 @@ static uint32_t tiles_across(uint32_t width, uint32_t shape) { return (width + (
 static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, uint32_t band_rows) {
     const uint32_t s44 = 2u | (2u << 4);
     PathLaunch g = {};
-    g.small_log2 = s44;
-    g.tiles_x_small = tiles_across(width, s44);
+    uint32_t small = s44;
+    {
+        const char* sv = getenv("WOLOLO_TILE_SMALL");
+        if (sv && *sv && shape_of(sv)) small = shape_of(sv);
+    }
+    g.small_log2 = small;
+    g.tiles_x_small = tiles_across(width, small);
+    const uint32_t sh = 1u << (small >> 4);
     double tail_rounds = 3.0;
     const char* tv = getenv("WOLOLO_TILE_TAIL");
     if (tv && *tv) tail_rounds = atof(tv);
@@ -1775,12 +1781,12 @@ static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, u
     g.tiles_x_big = tiles_across(width, big);
     const uint32_t bh = 1u << (big >> 4);
     uint32_t rows_small = 0;
-    if (tail_rounds > 0.0 && big != s44) {
+    if (tail_rounds > 0.0 && big != small) {
         uint64_t want = (uint64_t)(tail_rounds * resident + 0.5);
-        rows_small = (uint32_t)(((want + g.tiles_x_small - 1u) / g.tiles_x_small) * 4u);
+        rows_small = (uint32_t)(((want + g.tiles_x_small - 1u) / g.tiles_x_small) * sh);
     }
     uint32_t rows_big = rows > rows_small ? ((rows - rows_small) / bh) * bh : 0u;
-    if (big == s44) rows_big = ((rows + 3u) / 4u) * 4u;  // one shape: the big grid covers everything
+    if (big == small) rows_big = ((rows + bh - 1u) / bh) * bh;  // one shape: the big grid covers everything
     g.rows_big = rows_big;
     g.n_big = g.tiles_x_big * (rows_big / bh);
     return g;
@@ -1962,7 +1968,10 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
             tg.acc_spp = accum_spp;
         }
         const uint64_t n_small =
-            local_rows > tg.rows_big ? (uint64_t)tg.tiles_x_small * ((local_rows - tg.rows_big + 3u) / 4u) : 0u;
+            local_rows > tg.rows_big
+                ? (uint64_t)tg.tiles_x_small * ((local_rows - tg.rows_big + (1u << (tg.small_log2 >> 4)) - 1u) >>
+                                                (tg.small_log2 >> 4))
+                : 0u;
         const uint64_t n_wg = (uint64_t)tg.n_big + n_small;
         if (n_wg >= (1ull << 31)) {
             snprintf(err, errlen, "frame too large (%llu workgroups)", (unsigned long long)n_wg);
