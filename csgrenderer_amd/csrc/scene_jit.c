@@ -137,7 +137,7 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
                          "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oz) : \"v\"(o.z));\n"
                          "%*s  wodev::bound_tca_d2(ox, oy, oz, d, tca, d2);\n"
                          "%*s  asm(\"v_add_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(tr) : \"v\"(tca));\n"
-                         "%*s  const bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, bc3)) || (tr < 0.0f);\n"
+                         "%*s  const bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, bc3)) | (tr < 0.0f);\n"
                          "%*s  if (__ballot(!miss) == 0ull) cull[%u] |= %uu;\n"
                          "%*s}\n",
                          indent, "", indent, "", vb[0], indent, "", vb[1], indent, "", vb[2], indent, "", indent, "",
@@ -257,7 +257,7 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
              * bit at t_min; a re-collect keeps only the events after `after`. */
             if (g->first_pass)
                 bput(g->b,
-                     "%*s    bits[%u] |= ((iv.a <= tmin && iv.b > tmin) ? 1u : 0u) << %u;\n"
+                     "%*s    bits[%u] |= ((iv.a <= tmin) & (iv.b > tmin) ? 1u : 0u) << %u;\n"
                      "%*s    if (iv.a > tmin) { WO_WK(WO_WORK_EVENTS); win.insert(wodev::event_key_lo(iv.a, ka | iv.ma)); }\n"
                      "%*s    if ((iv.b > tmin) & (iv.b < wodev::kInf)) { WO_WK(WO_WORK_EVENTS); win.insert(wodev::event_key_lo(iv.b, kb | iv.mb)); }\n"
                      "%*s  }\n%*s}\n",
@@ -302,7 +302,7 @@ static void gen_lone_sphere(Gen* g, const WoRec* L, uint32_t ord, int indent) {
          indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", ord << 12, (ord << 12) | (1u << 11));
     if (g->first_pass)
         bput(g->b,
-             "%*s      bits[%u] |= ((la <= tmin && lb > tmin) ? 1u : 0u) << %u;\n"
+             "%*s      bits[%u] |= ((la <= tmin) & (lb > tmin) ? 1u : 0u) << %u;\n"
              "%*s      if (la > tmin) { WO_WK(WO_WORK_EVENTS); win.insert(wodev::event_key_lo(la, ka)); }\n"
              "%*s      if ((lb > tmin) & (lb < wodev::kInf)) { WO_WK(WO_WORK_EVENTS); win.insert(wodev::event_key_lo(lb, kb)); }\n",
              indent, "", ord / 32, ord % 32, indent, "", indent, "");
@@ -760,7 +760,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             bput(&b, "        r = v%u;\n      }\n", rv);
         }
         bput(&b,
-             "      if (have && r != root) { wodev::hit_from_key(key, r, hit); return true; }\n"
+             "      if (have & (r != root)) { wodev::hit_from_key(key, r, hit); return true; }\n"
              "      root = r;\n"
              "      if (!win.next(key)) {  // key keeps the last processed event\n"
              "        if (!win.dropped()) return false;\n"

@@ -415,13 +415,13 @@ struct LaneTracer {
         auto visit = [&](uint32_t ord, uint32_t& cnt) {
             const Ivl iv = prim_ivl(ord, o, d, inv, have_inv);
             if (!(iv.a > iv.b)) {
-                if (iv.a <= tmin && iv.b > tmin) ++cnt;
+                if ((iv.a <= tmin) & (iv.b > tmin)) ++cnt;
                 const uint64_t k0 = event_key(iv.a, ord, 0u, iv.ma), k1 = event_key(iv.b, ord, 1u, iv.mb);
-                if (iv.a > tmin && k0 > after) {
+                if ((iv.a > tmin) & (k0 > after)) {
                     WO_WK(WO_WORK_EVENTS);
                     best = k0 < best ? k0 : best;
                 }
-                if (iv.b > tmin && iv.b < kInf && k1 > after) {
+                if ((iv.b > tmin) & (iv.b < kInf) & (k1 > after)) {
                     WO_WK(WO_WORK_EVENTS);
                     best = k1 < best ? k1 : best;
                 }
@@ -449,10 +449,10 @@ struct LaneTracer {
                 const float tb = best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(best >> 32));
                 float fa, fb;
                 const float na = box_near(a0, a1, ri, oi, fa), nb = box_near(b0, b1, ri, oi, fb);
-                const bool ha = fa >= fmaxf(na, 0.0f) && na <= tb;
-                const bool hb = fb >= fmaxf(nb, 0.0f) && nb <= tb;
+                const bool ha = (fa >= fmaxf(na, 0.0f)) & (na <= tb);
+                const bool hb = (fb >= fmaxf(nb, 0.0f)) & (nb <= tb);
                 const uint32_t ra = __float_as_uint(a0.w), rb = __float_as_uint(a1.w);
-                if (ha && hb) {
+                if (ha & hb) {
                     const bool a_first = na <= nb;
                     cur = a_first ? ra : rb;
                     const uint32_t other = a_first ? rb : ra;
@@ -462,7 +462,7 @@ struct LaneTracer {
                     cur = ha ? ra : (hb ? rb : kNoRef);
                 }
             }
-            if (cur == kNoRef && sp != 0u) {
+            if ((cur == kNoRef) & (sp != 0u)) {
                 --sp;
                 cur = stk[sp * kBlock];
             }
