@@ -313,6 +313,9 @@ constexpr uint32_t kLeafRef = 0x80000000u, kNoRef = 0xffffffffu;
 // and the per-lane LDS stack holds as many entries as the built tree has levels:
 // a walk pushes at most one sibling per ancestor, so the stack never overflows.
 constexpr uint32_t kLaneDepthMax = 24;
+#ifndef WO_LANES_FUSED_SPHERE
+#define WO_LANES_FUSED_SPHERE 1
+#endif
 // dynamic LDS of the BVH walk (stacks + top nodes): with the kernel's static LDS,
 // 8 workgroups of kBlock fit in a CU's 160 KB
 constexpr size_t kLanesBvhLds = 18u * 1024u;
@@ -413,6 +416,35 @@ struct LaneTracer {
         const float tmin = WO_T_MIN;
         uint64_t best = kEmptyKey;
         auto visit = [&](uint32_t ord, uint32_t& cnt) {
+#if WO_LANES_FUSED_SPHERE
+            if constexpr (kSpheresOnly) {
+                // a sphere's interval [-b - s, -b + s] exists exactly when disc >= 0: the
+                // count and the events inside the sqrt branch, no empty interval formed
+                // (the specialised kernel's lone spheres; same bits as prim_ivl's form)
+                WO_WK(WO_WORK_SPHERE_TESTS);
+                const float4 g = lgeo[ord];
+                float b, ll;
+                sphere_bl(g.x, g.y, g.z, o, d, b, ll);
+                const float disc = g.w - ll;
+                if (__ballot(sphere_need(b, disc)) != 0ull) {
+                    asm volatile("");
+                    if (!(disc < 0.0f)) {
+                        const float s = sqrt_pt(disc), nb = -b, la = nb - s, lb = nb + s;
+                        if ((la <= tmin) & (lb > tmin)) ++cnt;
+                        const uint64_t k0 = event_key(la, ord, 0u, 0u), k1 = event_key(lb, ord, 1u, 0u);
+                        if ((la > tmin) & (k0 > after)) {
+                            WO_WK(WO_WORK_EVENTS);
+                            best = k0 < best ? k0 : best;
+                        }
+                        if ((lb > tmin) & (lb < kInf) & (k1 > after)) {
+                            WO_WK(WO_WORK_EVENTS);
+                            best = k1 < best ? k1 : best;
+                        }
+                    }
+                }
+                return;
+            }
+#endif
             const Ivl iv = prim_ivl(ord, o, d, inv, have_inv);
             if (!(iv.a > iv.b)) {
                 if ((iv.a <= tmin) & (iv.b > tmin)) ++cnt;
