@@ -94,6 +94,9 @@ typedef struct Gen {
     int lit_consts;   /* sphere / BOUND / axis-face constants as VALU literal operands instead of scalar moves */
     int first_event;  /* the first event of waves that start outside every primitive from a constant table */
     int fused_sphere; /* a lone sphere's membership and events inside its sqrt branch (no empty interval) */
+    int dl_eval;      /* chains of literal sets evaluated as decision lists (gen_eval_flat) */
+    struct DList* dls; /* decision-list pool (ids are 1-based; 0 = none) */
+    uint32_t ndl, dl_cap;
     int err;
 } Gen;
 
@@ -382,16 +385,160 @@ static uint32_t gen_eval(Gen* g, uint32_t start, uint32_t end, int indent) {
  * masks (SALU).  Same function of `bits` as gen_eval. */
 typedef struct Term {
     /* kind 0: the named bool v; kind 1: v & conj(P, N); kind 2: v | disj(P, N),
-     * v == kNoName meaning the literal set alone (an empty set is the identity) */
+     * v == kNoName meaning the literal set alone (an empty set is the identity).
+     * dl: the same value as a decision list (1-based id, 0 = none); cost: the
+     * rough VALU/SALU count of evaluating the term as written, for the choice
+     * between the two forms when it is named. */
     int kind;
     uint32_t w, P, N, v;
+    uint32_t dl, cost;
 } Term;
 
 enum { kNoName = 0xffffffffu };
 
+/* ---- decision lists ----
+ * A chain of set operations whose right operands are literal sets, e.g. the
+ * left-deep ((((a u b) \ c) u d) \ e) ... of csg256_chain, is a decision list:
+ * walking from the last operation down, a union operand that holds the point
+ * decides "inside", a subtracted one "outside", an intersected one that does NOT
+ * hold it "outside"; the first operand decides when nothing above it does.  When
+ * the operands' primitive ordinals grow along the chain (postfix order does
+ * that), the deciding entry is the highest set bit of
+ * (bits ^ INV) & USED, and its value a bit of VAL at that position: one
+ * count-leading-zeros and a shift per membership word instead of one mask
+ * compare and one lane-mask operation per chain link. */
+#define DL_WORDS 8
+typedef struct DList {
+    uint32_t used[DL_WORDS]; /* primitives in the list */
+    uint32_t inv[DL_WORDS];  /* entry decides when its primitive does NOT hold the point */
+    uint32_t val[DL_WORDS];  /* the value an entry decides */
+    int dflt;                /* the value when no entry decides */
+} DList;
+
+static uint32_t dl_new(Gen* g) {
+    if (g->ndl == g->dl_cap) {
+        uint32_t cap = g->dl_cap ? 2u * g->dl_cap : 64u;
+        DList* p = (DList*)realloc(g->dls, cap * sizeof(DList));
+        if (!p) {
+            g->err = 1;
+            return 0;
+        }
+        g->dls = p;
+        g->dl_cap = cap;
+    }
+    memset(&g->dls[g->ndl], 0, sizeof(DList));
+    return ++g->ndl;
+}
+
 static int term_is_literal(const Term* t) {
     uint32_t m = t->P | t->N;
     return t->kind && t->v == kNoName && m && (m & (m - 1u)) == 0u;
+}
+
+/* t as a decision list for a join of `kind` (1 intersection, 2 union): its own,
+ * or a literal set's (kind 2: any entry decides 1, else 0; kind 1: any entry
+ * decides 0, else 1; a single literal takes the join's form) */
+static uint32_t dl_of(Gen* g, const Term* t, int kind) {
+    if (t->dl) return t->dl;
+    if (!g->dl_eval || !t->kind || t->v != kNoName || !(t->P | t->N) || t->w >= DL_WORDS) return 0;
+    const int k = term_is_literal(t) ? kind : t->kind;
+    uint32_t id = dl_new(g);
+    if (!id) return 0;
+    DList* d = &g->dls[id - 1u];
+    d->used[t->w] = t->P | t->N;
+    if (k == 2) {
+        d->inv[t->w] = t->N;
+        d->val[t->w] = t->P | t->N;
+        d->dflt = 0;
+    } else {
+        d->inv[t->w] = t->P;
+        d->dflt = 1;
+    }
+    return id;
+}
+
+/* the join of `kind` with `top` above `base`.  A union's top must be a plain
+ * disjunction (every entry decides 1, default 0), an intersection's a plain
+ * conjunction (every entry decides 0, default 1): then whenever an entry of top
+ * decides, it decides the join.  Entries sit at their bit positions, so every
+ * entry of base above the lowest of top's must already decide the same value
+ * (their relative order then does not matter); otherwise no list. */
+static uint32_t dl_merge(Gen* g, uint32_t base, uint32_t top, int kind) {
+    if (!base || !top) return 0;
+    const int v = kind == 2;
+    const DList* t = &g->dls[top - 1u];
+    const DList* b = &g->dls[base - 1u];
+    if (t->dflt == v) return 0;
+    uint32_t lo = 0xffffffffu;
+    for (uint32_t w = 0; w < DL_WORDS; ++w) {
+        if ((t->val[w] & t->used[w]) != (v ? t->used[w] : 0u)) return 0;
+        if (b->used[w] & t->used[w]) return 0;
+        if (t->used[w] && lo == 0xffffffffu) lo = 32u * w + (uint32_t)__builtin_ctz(t->used[w]);
+    }
+    if (lo == 0xffffffffu) return 0;
+    for (uint32_t w = lo / 32u; w < DL_WORDS; ++w) {
+        const uint32_t above = w > lo / 32u ? ~0u : (lo % 32u == 31u ? 0u : ~0u << (lo % 32u + 1u));
+        if (b->used[w] & above & (v ? ~b->val[w] : b->val[w])) return 0;
+    }
+    uint32_t id = dl_new(g);
+    if (!id) return 0;
+    DList* d = &g->dls[id - 1u];
+    *d = g->dls[base - 1u];
+    t = &g->dls[top - 1u];
+    for (uint32_t w = 0; w < DL_WORDS; ++w) {
+        d->used[w] |= t->used[w];
+        d->inv[w] |= t->inv[w];
+        d->val[w] |= t->val[w];
+    }
+    return id;
+}
+
+static uint32_t dl_not(Gen* g, uint32_t id) {
+    if (!id) return 0;
+    uint32_t n = dl_new(g);
+    if (!n) return 0;
+    DList* d = &g->dls[n - 1u];
+    *d = g->dls[id - 1u];
+    for (uint32_t w = 0; w < DL_WORDS; ++w) d->val[w] ^= d->used[w];
+    d->dflt ^= 1;
+    return n;
+}
+
+static uint32_t dl_cost(const Gen* g, uint32_t id) {
+    const DList* d = &g->dls[id - 1u];
+    uint32_t c = 1;
+    for (uint32_t w = 0; w < DL_WORDS; ++w)
+        if (d->used[w]) c += 6u;
+    return c;
+}
+
+/* the list as a named bool: words from the lowest (least priority) up, each
+ * overriding the value where one of its entries decides */
+static uint32_t dl_name(Gen* g, uint32_t id, int indent) {
+    const DList* d = &g->dls[id - 1u];
+    uint32_t v = g->nval++;
+    bput(g->b, "%*sbool v%u = %s;  // decision list\n", indent, "", v, d->dflt ? "true" : "false");
+    for (uint32_t w = 0; w < DL_WORDS; ++w) {
+        const uint32_t u = d->used[w];
+        if (!u) continue;
+        char x[96];
+        if (d->inv[w])
+            snprintf(x, sizeof x, "((bits[%u] ^ 0x%08xu) & 0x%08xu)", w, d->inv[w], u);
+        else if (u != ~0u)
+            snprintf(x, sizeof x, "(bits[%u] & 0x%08xu)", w, u);
+        else
+            snprintf(x, sizeof x, "bits[%u]", w);
+        const uint32_t vals = d->val[w] & u;
+        if (vals == u)
+            bput(g->b, "%*sv%u = v%u | (%s != 0u);\n", indent, "", v, v, x);
+        else if (vals == 0u)
+            bput(g->b, "%*sv%u = v%u & (%s == 0u);\n", indent, "", v, v, x);
+        else
+            bput(g->b,
+                 "%*s{ const uint32_t dw = %s; v%u = dw != 0u ? (int32_t)(0x%08xu << __builtin_clz(dw)) < 0 : v%u; }\n",
+                 indent, "", x, v, vals, v);
+    }
+    return v;
 }
 
 /* the literal set of t (kind 1/2) as a named bool */
@@ -412,7 +559,11 @@ static uint32_t bool_op(Gen* g, uint32_t x, uint32_t y, int kind, int indent) {
 
 static uint32_t term_name(Gen* g, const Term* t, int indent) {
     if (t->kind == 0) return t->v;
-    if ((t->P | t->N) == 0u) {
+    const uint32_t m = t->P | t->N;
+    /* the decision list where it is cheaper than the term as written (a literal
+     * set adds an AND, a compare and a lane-mask operation) */
+    if (t->dl && dl_cost(g, t->dl) < t->cost + (m ? 3u : 0u)) return dl_name(g, t->dl, indent);
+    if (m == 0u) {
         if (t->v != kNoName) return t->v;
         uint32_t v = g->nval++;
         bput(g->b, "%*sconst bool v%u = %s;\n", indent, "", v, t->kind == 1 ? "true" : "false");
@@ -428,16 +579,23 @@ static Term term_not(Gen* g, Term t, int indent) {
         nv = g->nval++;
         bput(g->b, "%*sconst bool v%u = !v%u;\n", indent, "", nv, t.v);
     }
+    const uint32_t dl = dl_not(g, t.dl), cost = t.cost + (nv != kNoName);
     if (t.kind == 0) {
-        Term r = {0, 0, 0, 0, nv};
+        Term r = {0, 0, 0, 0, nv, dl, cost};
         return r;
     }
-    Term r = {t.kind == 1 ? 2 : 1, t.w, t.N, t.P, nv};
+    Term r = {t.kind == 1 ? 2 : 1, t.w, t.N, t.P, nv, dl, cost};
     return r;
 }
 
 /* kind 1: intersection, kind 2: union.  Literal sets of one bits word merge. */
 static Term term_join(Gen* g, Term a, Term b, int kind, int indent) {
+    /* the decision-list form: either operand as the list, the other (a literal
+     * set) on top of it */
+    const uint32_t da = dl_of(g, &a, kind), db = dl_of(g, &b, kind);
+    uint32_t dl = dl_merge(g, da, db, kind);
+    if (!dl) dl = dl_merge(g, db, da, kind);
+    const uint32_t nval0 = g->nval;
     Term x[2] = {a, b};
     for (int i = 0; i < 2; ++i) {
         if (x[i].kind == kind) continue;
@@ -446,10 +604,10 @@ static Term term_join(Gen* g, Term a, Term b, int kind, int indent) {
             continue;
         }
         uint32_t v = term_name(g, &x[i], indent);
-        Term n = {kind, 0, 0, 0, v};
+        Term n = {kind, 0, 0, 0, v, 0, 0};
         x[i] = n;
     }
-    Term r = {kind, x[0].w, x[0].P, x[0].N, kNoName};
+    Term r = {kind, x[0].w, x[0].P, x[0].N, kNoName, 0, 0};
     uint32_t m0 = x[0].P | x[0].N, m1 = x[1].P | x[1].N;
     uint32_t extra = kNoName;
     if (!m0) {
@@ -460,11 +618,13 @@ static Term term_join(Gen* g, Term a, Term b, int kind, int indent) {
         r.P |= x[1].P, r.N |= x[1].N;
     }
     r.v = bool_op(g, bool_op(g, x[0].v, x[1].v, kind, indent), extra, kind, indent);
+    r.dl = dl;
+    r.cost = a.cost + b.cost + 2u * (g->nval - nval0);
     return r;
 }
 
 static Term gen_eval_flat(Gen* g, uint32_t start, uint32_t end, int indent) {
-    Term stack[64], none = {0, 0, 0, 0, 0};
+    Term stack[64], none = {0, 0, 0, 0, 0, 0, 0};
     int sp = 0;
     uint32_t pc = start;
     while (pc < end && !g->err) {
@@ -477,7 +637,7 @@ static Term gen_eval_flat(Gen* g, uint32_t start, uint32_t end, int indent) {
             ++pc;
         } else if (r->op == WO_OP_BOUND) {
             uint32_t k = g->nbound++;
-            Term t = {0, 0, 0, 0, g->nval++};
+            Term t = {0, 0, 0, 0, g->nval++, 0, 1};
             bput(g->b, "%*sbool v%u = false;\n%*sif (!(cull[%u] & %uu)) {\n", indent, "", t.v, indent, "", k / 32,
                  1u << (k % 32));
             Term inner = gen_eval_flat(g, pc + 1, r->u0, indent + 2);
@@ -486,7 +646,7 @@ static Term gen_eval_flat(Gen* g, uint32_t start, uint32_t end, int indent) {
             stack[sp++] = t;
             pc = r->u0;
         } else if (r->op == WO_OP_PRIM) {
-            Term t = {1, r->u1 / 32u, 1u << (r->u1 % 32u), 0u, kNoName};
+            Term t = {1, r->u1 / 32u, 1u << (r->u1 % 32u), 0u, kNoName, 0, 0};
             stack[sp++] = t;
             pc += 1 + r->u0;
         } else {
@@ -630,6 +790,11 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         const char* v = getenv("WOLOLO_JIT_FLAT_EVAL");
         if (v && *v) g.flat_eval = v[0] != '0';
     }
+    g.dl_eval = 1;
+    {
+        const char* v = getenv("WOLOLO_JIT_DL_EVAL");
+        if (v && *v) g.dl_eval = v[0] != '0';
+    }
     uint32_t nbounds = 0;
     /* with the member skip, a bound around one convex primitive costs more than it
      * saves (csg32 4.87 / 4.87 ms with it, 4.83 / 4.82 without, same box) */
@@ -749,6 +914,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         bput(&b,
              "    for (;;) {\n"
              "      uint32_t r;\n"
+             "      // WO_EVAL_BEGIN (the root's value from bits[] and cull[]; tests/test_jit.py compiles it on the host)\n"
              "      {\n");
         g.nbound = 0;
         if (g.flat_eval) {
@@ -759,6 +925,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             uint32_t rv = gen_eval(&g, 0, n_recs, 8);
             bput(&b, "        r = v%u;\n      }\n", rv);
         }
+        bput(&b, "      // WO_EVAL_END\n");
         bput(&b,
              "      if (have & (r != root)) { wodev::hit_from_key(key, r, hit); return true; }\n"
              "      root = r;\n"
@@ -832,6 +999,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "#endif\n"
          "}\n",
          n_recs ? n_recs : 1u, n_mats_used, n_prims ? n_prims : 1u, n_recs * 8u, n_mats_used * 8u, n_prims);
+    free(g.dls);
     if (g.err || b.oom) {
         free(b.s);
         return NULL;

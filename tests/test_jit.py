@@ -198,3 +198,100 @@ def test_second_process_renders_csg256_without_compiling(tmp_path):
     assert runs[1]["origin"] == "disk" and runs[1]["sec"] < 0.5, runs
     assert runs[1]["sum"] == runs[0]["sum"]
     print(runs)
+
+
+def _chain_scene(r, n, ops, seed):
+    """A left-deep chain over n spheres, its operators cycling through `ops`."""
+    rng = np.random.default_rng(seed)
+    acc = r.sphere(1.0)
+    for i in range(1, n):
+        s = r.sphere(float(rng.uniform(0.2, 0.6)))
+        op = {"u": r.union, "d": r.difference, "i": r.intersection}[ops[i % len(ops)]]
+        acc = op(wl.arg(acc), wl.arg(s, tuple(float(x) for x in rng.uniform(-1.0, 1.0, 3))))
+    return acc
+
+
+def _random_tree(r, n, seed):
+    """A random binary tree over n spheres and half-spaces, random operators."""
+    rng = np.random.default_rng(seed)
+    items = []
+    for _ in range(n):
+        if rng.random() < 0.8:
+            items.append(r.sphere(float(rng.uniform(0.2, 0.8))))
+        else:
+            items.append(r.halfspace(tuple(float(x) for x in rng.normal(size=3))))
+    while len(items) > 1:
+        i = int(rng.integers(0, len(items) - 1))
+        a, b = items[i], items[i + 1]
+        op = (r.union, r.difference, r.intersection)[int(rng.integers(0, 3))]
+        items[i:i + 2] = [op(wl.arg(a), wl.arg(b, tuple(float(x) for x in rng.uniform(-1.0, 1.0, 3))))]
+    return items[0]
+
+
+def _program_value(prog, nrec, bits):
+    """The root's membership for each row of `bits` (n x words, uint32): the
+    postfix program evaluated directly (BOUND records change nothing)."""
+    st = []
+    pc = 0
+    while pc < nrec:
+        rec = prog[pc]
+        if rec.op == wl.WO_OP_PRIM:
+            st.append(((bits[:, rec.u1 // 32] >> np.uint32(rec.u1 % 32)) & np.uint32(1)).astype(bool))
+            pc += 1 + rec.u0
+            continue
+        if rec.op != wl.WO_OP_BOUND:
+            b, a = st.pop(), st.pop()
+            st.append({wl.WO_OP_UNION: a | b, wl.WO_OP_INTER: a & b, wl.WO_OP_DIFF: a & ~b,
+                       wl.WO_OP_RDIFF: b & ~a}[rec.op])
+        pc += 1
+    assert len(st) == 1
+    return st[0]
+
+
+@pytest.mark.parametrize("case", ["csg32", "csg256_balanced", "csg256_chain", "chain_uud", "chain_uid",
+                                  "chain_i", "chain_d", "random_a", "random_b"])
+@pytest.mark.parametrize("dl", ["1", "0"])
+def test_generated_root_evaluation(hostonly, monkeypatch, tmp_path, case, dl):
+    """The generated root evaluation (flattened literal sets, decision lists for
+    chains; WOLOLO_JIT_DL_EVAL) compiled on the host is the program's value for
+    random membership words of several densities and for every single primitive."""
+    import ctypes
+    import subprocess
+
+    monkeypatch.setenv("WOLOLO_JIT_DL_EVAL", dl)
+    r = wl.Renderer("eval", max_nodes=4096)
+    if case.startswith("csg"):
+        scenes.build(case, r)
+    elif case.startswith("chain"):
+        _chain_scene(r, {"chain_uud": 128, "chain_uid": 90, "chain_i": 40, "chain_d": 70}[case],
+                     case.split("_")[1], seed=len(case))
+    else:
+        _random_tree(r, 60 if case == "random_a" else 150, seed=ord(case[-1]))
+    prog, nrec, nprim = r.program()
+    src = r.jit_source()
+    r.close()
+    if dl == "1" and case in ("csg256_chain", "chain_uud", "chain_d"):
+        assert "decision list" in src  # left-deep unions / differences of spheres: one list
+    body = src[src.index("// WO_EVAL_BEGIN"):src.index("// WO_EVAL_END")]
+    nw = (nprim + 31) // 32
+    ncull = max(1, len(re.findall(r"cull\[(\d+)\] = 0u;", src)))
+    c = tmp_path / "ev.cpp"
+    c.write_text("#include <stddef.h>\n#include <stdint.h>\n"
+                 "extern \"C\" void run(const uint32_t* all, int n, uint32_t* out) {\n"
+                 f"  for (int i = 0; i < n; ++i) {{\n    const uint32_t* bits = all + (size_t)i * {nw};\n"
+                 f"    uint32_t cull[{ncull}] = {{0}};\n    uint32_t r;\n" + body + "    out[i] = r;\n  }\n}\n")
+    so = tmp_path / "ev.so"
+    subprocess.run(["g++", "-O1", "-shared", "-fPIC", "-o", str(so), str(c)], check=True)
+    lib = ctypes.CDLL(str(so))
+    rng = np.random.default_rng(7)
+    rows = [np.eye(nprim, dtype=np.uint8)]  # every primitive alone
+    for p in (0.01, 0.03, 0.1, 0.3, 0.5):
+        rows.append((rng.random((4000, nprim)) < p).astype(np.uint8))
+    mem = np.concatenate(rows)
+    bits = np.zeros((len(mem), nw), dtype=np.uint32)
+    for k in range(nprim):
+        bits[:, k // 32] |= mem[:, k].astype(np.uint32) << np.uint32(k % 32)
+    out = np.zeros(len(mem), dtype=np.uint32)
+    lib.run(bits.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(len(mem)), out.ctypes.data_as(ctypes.c_void_p))
+    want = _program_value(prog, nrec, bits)
+    assert np.array_equal(out.astype(bool), want), int(np.count_nonzero(out.astype(bool) != want))
