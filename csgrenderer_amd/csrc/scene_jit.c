@@ -535,7 +535,7 @@ static uint32_t dl_name(Gen* g, uint32_t id, int indent) {
             bput(g->b, "%*sv%u = v%u & (%s == 0u);\n", indent, "", v, v, x);
         else
             bput(g->b,
-                 "%*s{ const uint32_t dw = %s; v%u = dw != 0u ? (int32_t)(0x%08xu << __builtin_clz(dw)) < 0 : v%u; }\n",
+                 "%*s{ const uint32_t dw = %s; v%u = dw != 0u ? (int)(0x%08xu << __builtin_clz(dw)) < 0 : v%u; }\n",
                  indent, "", x, v, vals, v);
     }
     return v;

@@ -272,6 +272,7 @@ def test_generated_root_evaluation(hostonly, monkeypatch, tmp_path, case, dl):
     r.close()
     if dl == "1" and case in ("csg256_chain", "chain_uud", "chain_d"):
         assert "decision list" in src  # left-deep unions / differences of spheres: one list
+        assert wl.jit_compile_check(src, "gfx950") == ""  # and hiprtc takes it
     body = src[src.index("// WO_EVAL_BEGIN"):src.index("// WO_EVAL_END")]
     nw = (nprim + 31) // 32
     ncull = max(1, len(re.findall(r"cull\[(\d+)\] = 0u;", src)))

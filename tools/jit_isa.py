@@ -35,7 +35,7 @@ def main():
     shutil.copy(os.path.join(ROOT, "csgrenderer_amd/csrc/wo_device_common.h"), d)
     shutil.copy(os.path.join(ROOT, "include/wololo/wo_scene.h"), os.path.join(d, "wololo"))
     open(os.path.join(d, "k.hip"), "w").write("#include <hip/hip_runtime.h>\n" + src)
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-I", d, "-c",
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-I", d, "-c",
            os.path.join(d, "k.hip"), "--cuda-device-only", "-S", "-o", os.path.join(d, "k.s"),
            "-Rpass-analysis=kernel-resource-usage"] + [f"-D{x}" for x in a.D]
     res = subprocess.run(cmd, capture_output=True, text=True)
