@@ -95,6 +95,7 @@ typedef struct Gen {
     int first_event;  /* the first event of waves that start outside every primitive from a constant table */
     int fused_sphere; /* a lone sphere's membership and events inside its sqrt branch (no empty interval) */
     int dl_eval;      /* chains of literal sets evaluated as decision lists (gen_eval_flat) */
+    int union_count;  /* root a union of literal sets: a count of true terms kept per event */
     struct DList* dls; /* decision-list pool (ids are 1-based; 0 = none) */
     uint32_t ndl, dl_cap;
     int err;
@@ -673,6 +674,131 @@ static Term gen_eval_flat(Gen* g, uint32_t start, uint32_t end, int indent) {
     return stack[0];
 }
 
+/* ---- incremental union count ----
+ * When the root is a union of literal sets (each a conjunction or disjunction of
+ * primitive literals of one membership word), an event toggles one primitive,
+ * and only the one term holding that primitive can change: the sweep keeps the
+ * number of true terms and updates it from that term before and after the
+ * toggle (a table lookup and two mask compares), instead of re-evaluating every
+ * term per event.  The root is inside iff the count is > 0.  csg256_balanced's
+ * union of 65 pair terms is the case this is for. */
+typedef struct LSet {
+    int type;        /* 0 other, 1 literal set, 2 union of terms */
+    int kind;        /* literal set: 1 conj, 2 disj (a single literal is either) */
+    uint32_t w;      /* literal set: first membership word of its 64-bit window */
+    uint64_t P, N;   /* literal set: bit i = primitive 32 w + i */
+} LSet;
+
+typedef struct UTerm {
+    uint32_t w, neg; /* true iff ((window(w) & m) == q) != neg, window(w) = bits[w] | bits[w + 1] << 32 */
+    uint64_t m, q;
+} UTerm;
+
+static int lset_single(const LSet* a) {
+    uint64_t m = a->P | a->N;
+    return m && (m & (m - 1u)) == 0u;
+}
+
+static LSet lset_not(LSet a) {
+    LSet r = a;
+    r.kind = a.kind == 1 ? 2 : 1;
+    r.P = a.N;
+    r.N = a.P;
+    return r;
+}
+
+static void uterm_add(UTerm* t, uint32_t* nt, uint32_t cap, const LSet* a, int* ok) {
+    if (*nt >= cap) {
+        *ok = 0;
+        return;
+    }
+    UTerm u;
+    u.w = a->w;
+    u.m = a->P | a->N;
+    if (a->kind == 1 || lset_single(a)) {
+        u.q = a->P; /* conj: every P set, every N clear */
+        u.neg = 0;
+    } else {
+        u.q = a->N; /* disj: not (every P clear and every N set) */
+        u.neg = 1;
+    }
+    t[(*nt)++] = u;
+}
+
+/* join of two literal sets into one (kind 1 conj / 2 disj), when they fit one
+ * 64-bit window of the membership words */
+static int lset_merge(const LSet* a, const LSet* b, int kind, LSet* r) {
+    if (a->type != 1 || b->type != 1) return 0;
+    if ((a->kind != kind && !lset_single(a)) || (b->kind != kind && !lset_single(b))) return 0;
+    const LSet* lo = a->w <= b->w ? a : b;
+    const LSet* hi = a->w <= b->w ? b : a;
+    const uint32_t sh = 32u * (hi->w - lo->w);
+    if (sh > 32u || (sh && ((hi->P | hi->N) >> (64u - sh)) != 0u)) return 0;
+    const uint64_t hp = hi->P << sh, hn = hi->N << sh;
+    if ((lo->P | lo->N) & (hp | hn)) return 0;
+    r->type = 1;
+    r->kind = kind;
+    r->w = lo->w;
+    r->P = lo->P | hp;
+    r->N = lo->N | hn;
+    /* a set whose low word is empty moves its window up */
+    if (r->w + 1u && ((r->P | r->N) & 0xffffffffull) == 0u) {
+        r->w += 1u;
+        r->P >>= 32;
+        r->N >>= 32;
+    }
+    return 1;
+}
+
+/* the root's terms when it is a union of literal sets (0 terms otherwise) */
+static uint32_t union_terms(const WoRec* prog, uint32_t n_recs, uint32_t n_prims, UTerm* terms, uint32_t cap) {
+    LSet st[256];
+    uint32_t sp = 0, nt = 0;
+    int ok = 1;
+    for (uint32_t pc = 0; pc < n_recs && ok;) {
+        const WoRec* r = &prog[pc];
+        if (r->op == WO_OP_BOUND) {
+            ++pc;
+            continue;
+        }
+        if (r->op == WO_OP_PRIM) {
+            if (sp == 256u) return 0;
+            LSet a = {1, 1, r->u1 / 32u, 1ull << (r->u1 % 32u), 0u};
+            st[sp++] = a;
+            pc += 1u + r->u0;
+            continue;
+        }
+        if (sp < 2u) return 0;
+        LSet b = st[--sp], a = st[--sp], res = {0, 0, 0, 0, 0};
+        if (r->op == WO_OP_UNION) {
+            if (!lset_merge(&a, &b, 2, &res)) {
+                if (a.type == 0 || b.type == 0) {
+                    res.type = 0;
+                } else {
+                    if (a.type == 1) uterm_add(terms, &nt, cap, &a, &ok);
+                    if (b.type == 1) uterm_add(terms, &nt, cap, &b, &ok);
+                    res.type = 2;
+                }
+            }
+        } else if (a.type == 1 && b.type == 1) {
+            LSet x = a, y = b;
+            if (r->op == WO_OP_DIFF) y = lset_not(b);
+            if (r->op == WO_OP_RDIFF) {
+                x = b;
+                y = lset_not(a);
+            }
+            if (!lset_merge(&x, &y, 1, &res)) res.type = 0;
+        }
+        st[sp++] = res;
+        ++pc;
+    }
+    if (!ok || sp != 1u || st[0].type != 2) return 0;
+    /* every primitive in exactly one term */
+    uint32_t seen = 0;
+    for (uint32_t i = 0; i < nt; ++i) seen += (uint32_t)__builtin_popcountll(terms[i].m);
+    return seen == n_prims ? nt : 0u;
+}
+
 /* The root's membership when only primitive p holds the point: the postfix
  * program evaluated over bits = {p} (BOUND records do not change values). */
 static int single_root(const WoRec* prog, uint32_t n_recs, uint32_t p) {
@@ -721,6 +847,84 @@ static uint32_t tree_depth(const WoRec* prog, uint32_t n_recs) {
         }
     }
     return best;
+}
+
+/* The sweep for a root that is a union of literal-set terms (union_terms): the
+ * number of true terms at t_min (every term once; a culled BOUND's primitives
+ * stay 0, their true membership along the ray), then per event the toggled
+ * primitive's term before and after the toggle.  The root flips exactly when
+ * the count moves between 0 and non-zero. */
+static void gen_union_sweep(Gen* g, const UTerm* uterms, uint32_t n_uterms, uint32_t n_recs, uint32_t nw) {
+    Buf* b = g->b;
+    bput(b,
+         "    int ucnt = 0;  // true terms of the root's union\n"
+         "    if (!have) {\n"
+         "      uint32_t r;\n"
+         "      // WO_EVAL_BEGIN (the root's value from bits[] and cull[]; tests/test_jit.py compiles it on the host)\n"
+         "      {\n"
+         "        int c = 0;\n");
+    for (uint32_t i = 0; i < n_uterms; ++i) {
+        const UTerm* u = &uterms[i];
+        const uint32_t mlo = (uint32_t)u->m, mhi = (uint32_t)(u->m >> 32);
+        const uint32_t qlo = (uint32_t)u->q, qhi = (uint32_t)(u->q >> 32);
+        if (!mhi)
+            bput(b, "        c += (int)((bits[%u] & 0x%08xu) %s 0x%08xu);\n", u->w, mlo, u->neg ? "!=" : "==", qlo);
+        else
+            bput(b, "        c += (int)((((bits[%u] & 0x%08xu) == 0x%08xu) & ((bits[%u] & 0x%08xu) == 0x%08xu)) != %s);\n",
+                 u->w, mlo, qlo, u->w + 1u, mhi, qhi, u->neg ? "true" : "false");
+    }
+    bput(b,
+         "        ucnt = c;\n"
+         "        r = c != 0 ? 1u : 0u;\n"
+         "      }\n"
+         "      // WO_EVAL_END\n"
+         "      (void)r;\n"
+         "    }\n"
+         "    for (;;) {\n"
+         "      if (!win.next(key)) {  // key keeps the last processed event\n"
+         "        if (!win.dropped()) return false;\n"
+         "        after = key;\n"
+         "        WO_WK(WO_WORK_RECOLLECTS);\n"
+         "        win.clear();\n"
+         "        {\n");
+    g->nbound = 0;
+    g->first_pass = 0;
+    gen_collect(g, 0, n_recs, 10);
+    bput(b,
+         "        }\n"
+         "        if (!win.next(key)) return false;\n"
+         "      }\n"
+         "      WO_WK(WO_WORK_SWEEP_STEPS);\n"
+         "      WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);\n"
+         "      bool was;\n"
+         "      // WO_TOGGLE_BEGIN (the event's membership toggle; tests/test_jit.py)\n"
+         "      {\n"
+         "        const uint32_t ord = ((uint32_t)key) >> 12;\n"
+         "        const uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n"
+         "        const WoUTerm t = kUTerm[ord];\n");
+    if (nw == 1u) {
+        bput(b, "        const uint64_t cw = bits[0];\n");
+    } else {
+        bput(b, "        const uint32_t clo = ");
+        for (uint32_t w = 0; w + 1u < nw; ++w) bput(b, "t.w == %uu ? bits[%u] : ", w, w);
+        bput(b, "bits[%u];\n        const uint32_t chi = ", nw - 1u);
+        for (uint32_t w = 0; w + 2u < nw; ++w) bput(b, "t.w == %uu ? bits[%u] : ", w, w + 1u);
+        bput(b, "bits[%u];\n        const uint64_t cw = ((uint64_t)chi << 32) | clo;\n", nw - 1u);
+    }
+    bput(b,
+         "        const uint64_t tm = 1ull << (ord - 32u * t.w);\n"
+         "        const bool tb = ((cw & t.m) == t.q) != (t.neg != 0u);\n"
+         "        const bool ta = (((cw ^ tm) & t.m) == t.q) != (t.neg != 0u);\n"
+         "        was = ucnt != 0;\n"
+         "        ucnt += (int)ta - (int)tb;\n");
+    for (uint32_t w = 0; w < nw; ++w) bput(b, "        bits[%u] ^= w == %uu ? m : 0u;\n", w, w);
+    bput(b,
+         "      }\n"
+         "      // WO_TOGGLE_END\n"
+         "      if ((ucnt != 0) != was) { wodev::hit_from_key(key, ucnt != 0 ? 1u : 0u, hit); return true; }\n"
+         "    }\n"
+         "  }\n"
+         "};\n");
 }
 
 char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prims) {
@@ -790,6 +994,12 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         const char* v = getenv("WOLOLO_JIT_FLAT_EVAL");
         if (v && *v) g.flat_eval = v[0] != '0';
     }
+    /* incremental union count: 1 = when the root is a union of >= 12 literal-set terms, 2 = whenever it is one */
+    g.union_count = 1;
+    {
+        const char* v = getenv("WOLOLO_JIT_UNION_COUNT");
+        if (v && *v) g.union_count = (int)strtol(v, NULL, 10);
+    }
     g.dl_eval = 1;
     {
         const char* v = getenv("WOLOLO_JIT_DL_EVAL");
@@ -819,15 +1029,43 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         const char* v = getenv("WOLOLO_JIT_LDS_PROG");
         if (v && *v) lds_prog = v[0] != '0';
     }
-    /* the register window for deep trees holds 6 events (csg256 chain 29.5 ms at 4,
-     * 27.6 at 6, 27.5 at 8) */
-    if (!g.lds_events) bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW 6\n#endif\n");
+    /* the register window for deep trees holds 5 events (csg256 chain 29.5 ms at 4,
+     * 27.6 at 6, 27.5 at 8; with decision lists 19.36 at 4, 18.47 at 5, 18.65 at 6) */
+    if (!g.lds_events) bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW 5\n#endif\n");
     /* small scenes run 8 waves per SIMD: a 7-entry LDS list keeps 8 workgroups'
      * LDS within the CU (csg32 5.24 -> 5.19 ms; csg256 balanced keeps 8 entries:
      * 15.12 vs 15.33 ms at 7) */
     if (g.lds_events && n_prims <= 64u) bput(&b, "#ifndef WO_LDS_EVENTS\n#define WO_LDS_EVENTS 7\n#endif\n");
     bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
          g.lds_events, tree_depth(prog, n_recs), lds_prog);
+    /* the incremental union count's term table, per primitive: its term's mask test */
+    uint32_t n_uterms = 0;
+    UTerm* uterms = NULL;
+    if (g.union_count && n_prims) {
+        uterms = (UTerm*)malloc(sizeof(UTerm) * n_prims);
+        if (!uterms) g.err = 1;
+        else n_uterms = union_terms(prog, n_recs, n_prims, uterms, n_prims);
+        if (n_uterms < (g.union_count >= 2 ? 1u : 12u)) n_uterms = 0;
+    }
+    if (n_uterms) {
+        bput(&b, "struct __attribute__((aligned(16))) WoUTerm { uint64_t m, q; uint32_t w, neg, pad0, pad1; };\n");
+        bput(&b, "// root = union of %u literal-set terms: a term is true iff ((window(w) & m) == q) != neg,\n"
+                 "// window(w) = bits[w] | bits[w + 1] << 32; per primitive, the term it belongs to\n", n_uterms);
+        bput(&b, "__constant__ WoUTerm kUTerm[%u] = {", n_prims);
+        for (uint32_t p = 0; p < n_prims; ++p) {
+            const UTerm* u = NULL;
+            for (uint32_t i = 0; i < n_uterms && !u; ++i)
+                if (p >= 32u * uterms[i].w && p < 32u * uterms[i].w + 64u && ((uterms[i].m >> (p - 32u * uterms[i].w)) & 1u))
+                    u = &uterms[i];
+            if (!u) {
+                g.err = 1;
+                break;
+            }
+            bput(&b, "%s{0x%016llxull, 0x%016llxull, %uu, %uu, 0u, 0u}", p ? ", " : "", (unsigned long long)u->m,
+                 (unsigned long long)u->q, u->w, u->neg);
+        }
+        bput(&b, "};\n");
+    }
     bput(&b, "__constant__ uint32_t kOrdPc[%u] = {", n_prims ? n_prims : 1u);
     if (!n_prims) bput(&b, "0u");
     for (uint32_t i = 0, o = 0; i < n_recs; ++i)
@@ -911,49 +1149,56 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  "      have = true;  // root stays 0\n"
                  "    }\n");
         }
-        bput(&b,
-             "    for (;;) {\n"
-             "      uint32_t r;\n"
-             "      // WO_EVAL_BEGIN (the root's value from bits[] and cull[]; tests/test_jit.py compiles it on the host)\n"
-             "      {\n");
-        g.nbound = 0;
-        if (g.flat_eval) {
-            Term rt = gen_eval_flat(&g, 0, n_recs, 8);
-            uint32_t rv = term_name(&g, &rt, 8);
-            bput(&b, "        r = v%u ? 1u : 0u;\n      }\n", rv);
+        if (n_uterms) {
+            gen_union_sweep(&g, uterms, n_uterms, n_recs, nw);
         } else {
-            uint32_t rv = gen_eval(&g, 0, n_recs, 8);
-            bput(&b, "        r = v%u;\n      }\n", rv);
+            bput(&b,
+                 "    for (;;) {\n"
+                 "      uint32_t r;\n");
+            bput(&b,
+                 "      // WO_EVAL_BEGIN (the root's value from bits[] and cull[]; tests/test_jit.py compiles it on the host)\n"
+                 "      {\n");
+            g.nbound = 0;
+            if (g.flat_eval) {
+                Term rt = gen_eval_flat(&g, 0, n_recs, 8);
+                uint32_t rv = term_name(&g, &rt, 8);
+                bput(&b, "        r = v%u ? 1u : 0u;\n      }\n", rv);
+            } else {
+                uint32_t rv = gen_eval(&g, 0, n_recs, 8);
+                bput(&b, "        r = v%u;\n      }\n", rv);
+            }
+            bput(&b, "      // WO_EVAL_END\n");
+            bput(&b,
+                 "      if (have & (r != root)) { wodev::hit_from_key(key, r, hit); return true; }\n"
+                 "      root = r;\n"
+                 "      if (!win.next(key)) {  // key keeps the last processed event\n"
+                 "        if (!win.dropped()) return false;\n"
+                 "        after = key;\n"
+                 "        WO_WK(WO_WORK_RECOLLECTS);\n"
+                 "        win.clear();\n"
+                 "        {\n");
+            g.nbound = 0;
+            g.first_pass = 0;
+            gen_collect(&g, 0, n_recs, 10);
+            bput(&b,
+                 "        }\n"
+                 "        if (!win.next(key)) return false;\n"
+                 "      }\n"
+                 "      have = true;\n"
+                 "      WO_WK(WO_WORK_SWEEP_STEPS);\n"
+                     "      WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);\n"
+                 "      // WO_TOGGLE_BEGIN (the event's membership toggle; tests/test_jit.py)\n"
+                 "      {\n"
+                 "        uint32_t ord = ((uint32_t)key) >> 12;\n"
+                 "        uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n");
+            for (uint32_t w = 0; w < nw; ++w) bput(&b, "        bits[%u] ^= w == %uu ? m : 0u;\n", w, w);
+            bput(&b,
+                 "      }\n"
+                 "      // WO_TOGGLE_END\n"
+                 "    }\n"
+                 "  }\n"
+                 "};\n");
         }
-        bput(&b, "      // WO_EVAL_END\n");
-        bput(&b,
-             "      if (have & (r != root)) { wodev::hit_from_key(key, r, hit); return true; }\n"
-             "      root = r;\n"
-             "      if (!win.next(key)) {  // key keeps the last processed event\n"
-             "        if (!win.dropped()) return false;\n"
-             "        after = key;\n"
-             "        WO_WK(WO_WORK_RECOLLECTS);\n"
-             "        win.clear();\n"
-             "        {\n");
-        g.nbound = 0;
-        g.first_pass = 0;
-        gen_collect(&g, 0, n_recs, 10);
-        bput(&b,
-             "        }\n"
-             "        if (!win.next(key)) return false;\n"
-             "      }\n"
-             "      have = true;\n"
-             "      WO_WK(WO_WORK_SWEEP_STEPS);\n"
-                 "      WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);\n"
-             "      {\n"
-             "        uint32_t ord = ((uint32_t)key) >> 12;\n"
-             "        uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n");
-        for (uint32_t w = 0; w < nw; ++w) bput(&b, "        bits[%u] ^= w == %uu ? m : 0u;\n", w, w);
-        bput(&b,
-             "      }\n"
-             "    }\n"
-             "  }\n"
-             "};\n");
     }
     /* Waves per SIMD the register budget is sized for (measured, 1920x1080x64):
      * csg256 balanced / chain (128 primitives) 23.7 / 38.0 ms at 6, 21.3 / 33.8 at
@@ -1000,6 +1245,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "}\n",
          n_recs ? n_recs : 1u, n_mats_used, n_prims ? n_prims : 1u, n_recs * 8u, n_mats_used * 8u, n_prims);
     free(g.dls);
+    free(uterms);
     if (g.err || b.oom) {
         free(b.s);
         return NULL;

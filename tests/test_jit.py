@@ -248,51 +248,117 @@ def _program_value(prog, nrec, bits):
     return st[0]
 
 
-@pytest.mark.parametrize("case", ["csg32", "csg256_balanced", "csg256_chain", "chain_uud", "chain_uid",
-                                  "chain_i", "chain_d", "random_a", "random_b"])
-@pytest.mark.parametrize("dl", ["1", "0"])
-def test_generated_root_evaluation(hostonly, monkeypatch, tmp_path, case, dl):
-    """The generated root evaluation (flattened literal sets, decision lists for
-    chains; WOLOLO_JIT_DL_EVAL) compiled on the host is the program's value for
-    random membership words of several densities and for every single primitive."""
-    import ctypes
-    import subprocess
-
-    monkeypatch.setenv("WOLOLO_JIT_DL_EVAL", dl)
-    r = wl.Renderer("eval", max_nodes=4096)
+def _build_case(r, case):
     if case.startswith("csg"):
         scenes.build(case, r)
     elif case.startswith("chain"):
         _chain_scene(r, {"chain_uud": 128, "chain_uid": 90, "chain_i": 40, "chain_d": 70}[case],
                      case.split("_")[1], seed=len(case))
+    elif case.startswith("unionpairs"):
+        _union_of_pairs(r, 100 if case == "unionpairs" else 30, seed=5)
     else:
         _random_tree(r, 60 if case == "random_a" else 150, seed=ord(case[-1]))
-    prog, nrec, nprim = r.program()
-    src = r.jit_source()
-    r.close()
-    if dl == "1" and case in ("csg256_chain", "chain_uud", "chain_d"):
-        assert "decision list" in src  # left-deep unions / differences of spheres: one list
-        assert wl.jit_compile_check(src, "gfx950") == ""  # and hiprtc takes it
+
+
+def _union_of_pairs(r, n, seed):
+    """A balanced union of n pairs (a op b, op cycling u/d/i) -- csg256_balanced's shape."""
+    rng = np.random.default_rng(seed)
+    items = []
+    for i in range(n):
+        a, b = r.sphere(float(rng.uniform(0.3, 0.6))), r.sphere(float(rng.uniform(0.3, 0.6)))
+        op = (r.union, r.difference, r.intersection)[i % 3]
+        items.append(op(wl.arg(a), wl.arg(b, (0.2, 0.1, 0.0))))
+    while len(items) > 1:
+        items = [r.union(wl.arg(items[i]), wl.arg(items[i + 1], tuple(float(x) for x in rng.uniform(-2, 2, 3))))
+                 if i + 1 < len(items) else items[i] for i in range(0, len(items), 2)]
+    return items[0]
+
+
+def _compile_sweep(tmp_path, src, nw, ncull):
+    """The generated evaluation and toggle blocks (and the union-count table) as a
+    host function: evaluate at the start membership, then apply toggles, writing
+    the root after each."""
+    import ctypes
+    import subprocess
+
     body = src[src.index("// WO_EVAL_BEGIN"):src.index("// WO_EVAL_END")]
-    nw = (nprim + 31) // 32
-    ncull = max(1, len(re.findall(r"cull\[(\d+)\] = 0u;", src)))
+    toggle = src[src.index("// WO_TOGGLE_BEGIN"):src.index("// WO_TOGGLE_END")]
+    table = ""
+    m = re.search(r"struct __attribute__\(\(aligned\(16\)\)\) WoUTerm \{[^}]*\};", src)
+    if m:
+        t = re.search(r"__constant__ WoUTerm kUTerm\[\d+\] = \{.*?\};", src, re.S)
+        table = m.group(0) + "\n" + t.group(0).replace("__constant__", "static const") + "\n"
+        assert "ucnt" in toggle
+    root_after = "(ucnt != 0)" if table else None
     c = tmp_path / "ev.cpp"
-    c.write_text("#include <stddef.h>\n#include <stdint.h>\n"
-                 "extern \"C\" void run(const uint32_t* all, int n, uint32_t* out) {\n"
-                 f"  for (int i = 0; i < n; ++i) {{\n    const uint32_t* bits = all + (size_t)i * {nw};\n"
-                 f"    uint32_t cull[{ncull}] = {{0}};\n    uint32_t r;\n" + body + "    out[i] = r;\n  }\n}\n")
+    c.write_text("#include <stddef.h>\n#include <stdint.h>\n" + table +
+                 "extern \"C\" void run(const uint32_t* all, int n, const uint32_t* ords, int nev, uint32_t* out) {\n"
+                 f"  for (int i = 0; i < n; ++i) {{\n    uint32_t bits[{nw}];\n"
+                 f"    for (int k = 0; k < {nw}; ++k) bits[k] = all[(size_t)i * {nw} + k];\n"
+                 f"    uint32_t cull[{ncull}] = {{0}};\n    int ucnt = 0; (void)ucnt; bool was = false; (void)was;\n    uint32_t r;\n" + body +
+                 "    out[(size_t)i * (nev + 1)] = r;\n"
+                 "    for (int e = 0; e < nev; ++e) {\n"
+                 "      const uint64_t key = (uint64_t)ords[(size_t)i * nev + e] << 12;\n" + toggle +
+                 ("      out[(size_t)i * (nev + 1) + e + 1] = " + (root_after or "0") + ";\n") +
+                 "    }\n  }\n}\n")
     so = tmp_path / "ev.so"
     subprocess.run(["g++", "-O1", "-shared", "-fPIC", "-o", str(so), str(c)], check=True)
     lib = ctypes.CDLL(str(so))
+    return lib, table != ""
+
+
+@pytest.mark.parametrize("case", ["csg32", "csg256_balanced", "csg256_chain", "chain_uud", "chain_uid",
+                                  "chain_i", "chain_d", "random_a", "random_b", "unionpairs", "unionpairs_s"])
+@pytest.mark.parametrize("knobs", [{}, {"WOLOLO_JIT_DL_EVAL": "0", "WOLOLO_JIT_UNION_COUNT": "0"},
+                                   {"WOLOLO_JIT_UNION_COUNT": "2"}])
+def test_generated_root_evaluation(hostonly, monkeypatch, tmp_path, case, knobs):
+    """The generated root evaluation (flattened literal sets; decision lists for
+    chains, WOLOLO_JIT_DL_EVAL; the incremental count of a union of literal sets,
+    WOLOLO_JIT_UNION_COUNT) compiled on the host is the program's value for random
+    membership words of several densities and for every single primitive, and --
+    with the union count -- after each of a run of toggles (the sweep's events)."""
+    import ctypes
+
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    r = wl.Renderer("eval", max_nodes=4096)
+    _build_case(r, case)
+    prog, nrec, nprim = r.program()
+    src = r.jit_source()
+    r.close()
+    if not knobs and case in ("csg256_chain", "chain_uud", "chain_d"):
+        assert "decision list" in src  # left-deep unions / differences of spheres: one list
+        assert wl.jit_compile_check(src, "gfx950") == ""  # and hiprtc takes it
+    if not knobs and case in ("csg256_balanced", "unionpairs"):
+        assert "kUTerm" in src  # a union of >= 12 literal-set terms: the incremental count
+        assert wl.jit_compile_check(src, "gfx950") == ""
+    nw = (nprim + 31) // 32
+    ncull = max(1, len(re.findall(r"cull\[(\d+)\] = 0u;", src)))
+    lib, counted = _compile_sweep(tmp_path, src, nw, ncull)
     rng = np.random.default_rng(7)
-    rows = [np.eye(nprim, dtype=np.uint8)]  # every primitive alone
+    rows = [np.eye(nprim, dtype=np.uint8), np.zeros((1, nprim), dtype=np.uint8)]  # every primitive alone
     for p in (0.01, 0.03, 0.1, 0.3, 0.5):
-        rows.append((rng.random((4000, nprim)) < p).astype(np.uint8))
+        rows.append((rng.random((2000, nprim)) < p).astype(np.uint8))
     mem = np.concatenate(rows)
-    bits = np.zeros((len(mem), nw), dtype=np.uint32)
-    for k in range(nprim):
-        bits[:, k // 32] |= mem[:, k].astype(np.uint32) << np.uint32(k % 32)
-    out = np.zeros(len(mem), dtype=np.uint32)
-    lib.run(bits.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(len(mem)), out.ctypes.data_as(ctypes.c_void_p))
-    want = _program_value(prog, nrec, bits)
-    assert np.array_equal(out.astype(bool), want), int(np.count_nonzero(out.astype(bool) != want))
+    nev = 12 if counted else 0
+    ords = rng.integers(0, nprim, size=(len(mem), max(nev, 1)), dtype=np.uint32)
+    # a third of the rows toggle primitives of one neighbourhood (events of one term and its neighbours)
+    ords[::3] = (ords[::3, :1] + rng.integers(0, 3, size=(len(ords[::3]), ords.shape[1]))) % nprim
+
+    def pack(m):
+        bits = np.zeros((len(m), nw), dtype=np.uint32)
+        for k in range(nprim):
+            bits[:, k // 32] |= m[:, k].astype(np.uint32) << np.uint32(k % 32)
+        return bits
+
+    out = np.zeros((len(mem), nev + 1), dtype=np.uint32)
+    lib.run(pack(mem).ctypes.data_as(ctypes.c_void_p), ctypes.c_int(len(mem)),
+            np.ascontiguousarray(ords).ctypes.data_as(ctypes.c_void_p), ctypes.c_int(nev),
+            out.ctypes.data_as(ctypes.c_void_p))
+    cur = mem.copy()
+    for e in range(nev + 1):
+        if e:
+            cur[np.arange(len(cur)), ords[:, e - 1]] ^= 1
+        want = _program_value(prog, nrec, pack(cur))
+        got = out[:, e].astype(bool)
+        assert np.array_equal(got, want), (e, int(np.count_nonzero(got != want)))

@@ -24,12 +24,16 @@ def main():
     ap.add_argument("-D", action="append", default=[])
     ap.add_argument("--hist", action="store_true")
     ap.add_argument("--keep", default=None, help="copy the .s here")
+    ap.add_argument("--src", default=None, help="compile this (edited) generated source instead of the scene's")
+    ap.add_argument("--dump", default=None, help="write the scene's generated source here")
     a = ap.parse_args()
     from csgrenderer_amd import scenes
     from csgrenderer_amd import wololo as wl
     r = wl.Renderer("isa", max_nodes=4096)
     scenes.build(a.scene, r)
-    src = r.jit_source()
+    src = open(a.src).read() if a.src else r.jit_source()
+    if a.dump:
+        open(a.dump, "w").write(src)
     d = tempfile.mkdtemp()
     os.makedirs(os.path.join(d, "wololo"))
     shutil.copy(os.path.join(ROOT, "csgrenderer_amd/csrc/wo_device_common.h"), d)
