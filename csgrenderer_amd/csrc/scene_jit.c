@@ -994,7 +994,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         const char* v = getenv("WOLOLO_JIT_FLAT_EVAL");
         if (v && *v) g.flat_eval = v[0] != '0';
     }
-    /* incremental union count: 1 = when the root is a union of >= 12 literal-set terms, 2 = whenever it is one */
+    /* incremental union count: 1 = when the root is a union of >= 8 literal-set terms (csg32: 9 terms, 3.73 -> 3.68 ms), 2 = whenever it is one */
     g.union_count = 1;
     {
         const char* v = getenv("WOLOLO_JIT_UNION_COUNT");
@@ -1045,7 +1045,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         uterms = (UTerm*)malloc(sizeof(UTerm) * n_prims);
         if (!uterms) g.err = 1;
         else n_uterms = union_terms(prog, n_recs, n_prims, uterms, n_prims);
-        if (n_uterms < (g.union_count >= 2 ? 1u : 12u)) n_uterms = 0;
+        if (n_uterms < (g.union_count >= 2 ? 1u : 8u)) n_uterms = 0;
     }
     if (n_uterms) {
         bput(&b, "struct __attribute__((aligned(16))) WoUTerm { uint64_t m, q; uint32_t w, neg, pad0, pad1; };\n");

@@ -1,16 +1,10 @@
 #!/usr/bin/env bash
-# Round-2 A/B session: incremental union count (csg256 balanced, WOLOLO_JIT_UNION_COUNT) and the
-# deep-tree register window size (chain).
+# Round-2 session: full GPU suite with the current kernels, csg32 with the union count forced.
 S=tools/gpu_session.sh
-B="python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-count-work"
+B="python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-count-work"
 bash $S \
- "bal_uc:200:$B --scene csg256_balanced > gpurun_out/ab_bal_uc.json" \
- "bal_nouc:200:WOLOLO_JIT_UNION_COUNT=0 $B --scene csg256_balanced > gpurun_out/ab_bal_nouc.json" \
- "bal_uc2:200:$B --scene csg256_balanced > gpurun_out/ab_bal_uc2.json" \
- "bal_nouc2:200:WOLOLO_JIT_UNION_COUNT=0 $B --scene csg256_balanced > gpurun_out/ab_bal_nouc2.json" \
- "chain_w6:200:$B --scene csg256_chain > gpurun_out/ab_chain_w6.json" \
- "chain_w5:200:WOLOLO_JIT_FLAGS=-DWO_WINDOW=5 $B --scene csg256_chain > gpurun_out/ab_chain_w5.json" \
- "chain_w4:200:WOLOLO_JIT_FLAGS=-DWO_WINDOW=4 $B --scene csg256_chain > gpurun_out/ab_chain_w4.json" \
- "chain_w5b:200:WOLOLO_JIT_FLAGS=-DWO_WINDOW=5 $B --scene csg256_chain > gpurun_out/ab_chain_w5b.json" \
- "chain_w6b:200:$B --scene csg256_chain > gpurun_out/ab_chain_w6b.json" \
- "par:400:python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k 'balanced'"
+ "gt:700:python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
+ "c32:200:$B > gpurun_out/ab_c32.json" \
+ "c32_uc:200:WOLOLO_JIT_UNION_COUNT=2 $B > gpurun_out/ab_c32_uc.json" \
+ "c32b:200:$B > gpurun_out/ab_c32b.json" \
+ "c32_ucb:200:WOLOLO_JIT_UNION_COUNT=2 $B > gpurun_out/ab_c32_ucb.json"
