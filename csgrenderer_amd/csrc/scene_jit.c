@@ -863,8 +863,24 @@ static void gen_union_sweep(Gen* g, const UTerm* uterms, uint32_t n_uterms, uint
          "      // WO_EVAL_BEGIN (the root's value from bits[] and cull[]; tests/test_jit.py compiles it on the host)\n"
          "      {\n"
          "        int c = 0;\n");
+    /* terms that are one primitive: a population count per word (as separate
+     * compares the compiler extracted every bit first and spilled them) */
+    uint32_t single[64] = {0};
     for (uint32_t i = 0; i < n_uterms; ++i) {
         const UTerm* u = &uterms[i];
+        if (u->m == u->q && (u->m & (u->m - 1u)) == 0u && !u->neg) {
+            const uint32_t bit = 32u * u->w + (uint32_t)__builtin_ctzll(u->m);
+            if (bit / 32u < 64u) single[bit / 32u] |= 1u << (bit % 32u);
+        }
+    }
+    for (uint32_t w = 0; w < nw && w < 64u; ++w)
+        if (single[w]) bput(b, "        c += __builtin_popcount(bits[%u] & 0x%08xu);\n", w, single[w]);
+    for (uint32_t i = 0; i < n_uterms; ++i) {
+        const UTerm* u = &uterms[i];
+        if (u->m == u->q && (u->m & (u->m - 1u)) == 0u && !u->neg) {
+            const uint32_t bit = 32u * u->w + (uint32_t)__builtin_ctzll(u->m);
+            if (bit / 32u < 64u) continue;
+        }
         const uint32_t mlo = (uint32_t)u->m, mhi = (uint32_t)(u->m >> 32);
         const uint32_t qlo = (uint32_t)u->q, qhi = (uint32_t)(u->q >> 32);
         if (!mhi)
