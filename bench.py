@@ -19,6 +19,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -228,10 +229,16 @@ def main():
                     "brute_force_achieved": round(brute_tf, 3),
                     "brute_force_frac": round(brute_tf / PEAK_FP32_TFLOPS, 4)}
             if work is not None:
-                ex = executed_flop(work, info, r.trace_path())
+                eval_ops = None
+                if r.trace_path() == "jit":
+                    m = re.search(r"// wo_eval_ops_per_event (\d+)", r.jit_source() or "")
+                    eval_ops = int(m.group(1)) if m else None
+                ex = executed_flop(work, info, r.trace_path(), eval_ops)
                 ex_tf = ex / work["segments"] * seg_launch / (k_ms * 1e-3) / 1e12
                 roof.update({"achieved": round(ex_tf, 3), "frac": round(ex_tf / PEAK_FP32_TFLOPS, 4),
-                             "basis": "executed work (counted tests priced per SURVEY.md 8(d))",
+                             "basis": "executed work (counted tests priced per SURVEY.md 8(d); a swept event "
+                                      "priced at the emitted root evaluation's operations"
+                                      + (f", {eval_ops} per event)" if eval_ops else ")"),
                              "executed_flop_per_segment": round(ex / work["segments"], 2),
                              "work_per_segment": {k: round(v / work["segments"], 4) for k, v in work.items()
                                                   if k != "segments" and not k.startswith("cyc_")}})
@@ -289,9 +296,12 @@ def main():
 # SURVEY.md 8(d) prices: ray-sphere test 30 flop, ray-half-space 12, CSG combine 4 per
 # binop (one root evaluation per swept event; the lane tracer's union count is one
 # update), shading + scatter 40 per segment.  A BOUND test is the sphere test's
-# centre-to-line part without the root: priced 20.
-def executed_flop(work, info, path):
-    combine = 4 if path == "lanes" else 4 * info.binops
+# centre-to-line part without the root: priced 20.  The specialised kernel states the
+# operations its root evaluation runs per swept event (masked compares, a decision
+# list or the union count's update: `eval_ops`, scene_jit.c), which replaces the
+# 4-per-binop price where it is known.
+def executed_flop(work, info, path, eval_ops=None):
+    combine = 4 if path == "lanes" else (eval_ops if eval_ops else 4 * info.binops)
     return (30 * work["sphere_tests"] + 12 * work["halfspace_tests"] + 20 * work["bound_tests"]
             + combine * work["sweep_steps"] + 40 * work["segments"])
 

@@ -642,6 +642,12 @@ static Term gen_eval_flat(Gen* g, uint32_t start, uint32_t end, int indent) {
             bput(g->b, "%*sbool v%u = false;\n%*sif (!(cull[%u] & %uu)) {\n", indent, "", t.v, indent, "", k / 32,
                  1u << (k % 32));
             Term inner = gen_eval_flat(g, pc + 1, r->u0, indent + 2);
+            {
+                /* the cost of the form term_name picks, plus the cull test */
+                const uint32_t lits = inner.kind && (inner.P | inner.N) ? 3u : 0u;
+                const uint32_t dc = inner.dl ? dl_cost(g, inner.dl) : 0xffffffffu;
+                t.cost = 1u + (dc < inner.cost + lits ? dc : inner.cost + lits);
+            }
             uint32_t iv = term_name(g, &inner, indent + 2);
             bput(g->b, "%*s  v%u = v%u;\n%*s}\n", indent, "", t.v, iv, indent, "");
             stack[sp++] = t;
@@ -1055,7 +1061,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
          g.lds_events, tree_depth(prog, n_recs), lds_prog);
     /* the incremental union count's term table, per primitive: its term's mask test */
-    uint32_t n_uterms = 0;
+    uint32_t n_uterms = 0, eval_ops = 0;
     UTerm* uterms = NULL;
     if (g.union_count && n_prims) {
         uterms = (UTerm*)malloc(sizeof(UTerm) * n_prims);
@@ -1167,6 +1173,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         }
         if (n_uterms) {
             gen_union_sweep(&g, uterms, n_uterms, n_recs, nw);
+            eval_ops = 12u + 2u * (nw - 1u);
         } else {
             bput(&b,
                  "    for (;;) {\n"
@@ -1177,6 +1184,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             g.nbound = 0;
             if (g.flat_eval) {
                 Term rt = gen_eval_flat(&g, 0, n_recs, 8);
+                const uint32_t m = rt.kind ? (rt.P | rt.N) : 0u;
+                eval_ops = rt.dl && dl_cost(&g, rt.dl) < rt.cost + (m ? 3u : 0u) ? dl_cost(&g, rt.dl)
+                                                                                 : rt.cost + (m ? 3u : 0u);
                 uint32_t rv = term_name(&g, &rt, 8);
                 bput(&b, "        r = v%u ? 1u : 0u;\n      }\n", rv);
             } else {
@@ -1260,6 +1270,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "#endif\n"
          "}\n",
          n_recs ? n_recs : 1u, n_mats_used, n_prims ? n_prims : 1u, n_recs * 8u, n_mats_used * 8u, n_prims);
+    /* the root evaluation's operation count per swept event, for bench.py's
+     * executed-work roofline (0: not known, e.g. the postfix form) */
+    if (eval_ops) bput(&b, "// wo_eval_ops_per_event %u\n", eval_ops);
     free(g.dls);
     free(uterms);
     if (g.err || b.oom) {
