@@ -16,6 +16,7 @@
  */
 #include <inttypes.h>
 #include <stdarg.h>
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -96,6 +97,10 @@ typedef struct Gen {
     int fused_sphere; /* a lone sphere's membership and events inside its sqrt branch (no empty interval) */
     int dl_eval;      /* chains of literal sets evaluated as decision lists (gen_eval_flat) */
     int union_count;  /* root a union of literal sets: a count of true terms kept per event */
+    int spatial;      /* collect grouped by a spatial hierarchy over the primitives (gen_spatial) */
+    uint32_t spatial_leaf; /* most primitives in a leaf group of that hierarchy */
+    struct SPrim* sprims;  /* the bounded primitives it groups */
+    uint32_t nsprims;
     struct DList* dls; /* decision-list pool (ids are 1-based; 0 = none) */
     uint32_t ndl, dl_cap;
     int err;
@@ -106,6 +111,7 @@ typedef struct Gen {
  * primitive's own first member, with the member skip, is the cheaper test. */
 static int bound_tested(const Gen* g, uint32_t pc) {
     const WoRec* r = &g->prog[pc];
+    if (g->spatial) return 0; /* the spatial hierarchy culls instead (gen_spatial) */
     if (r->u1 < g->bound_min_leaves) return 0;
     if (!g->bound_single && pc + 1u < g->n && g->prog[pc + 1u].op == WO_OP_PRIM &&
         pc + 2u + g->prog[pc + 1u].u0 == r->u0)
@@ -317,6 +323,164 @@ static void gen_lone_sphere(Gen* g, const WoRec* L, uint32_t ord, int indent) {
              "%*s      if ((lb > tmin) & (lb < wodev::kInf) & (k1 > after)) { WO_WK(WO_WORK_EVENTS); win.insert(k1); }\n",
              indent, "", indent, "", indent, "");
     bput(g->b, "%*s    }\n%*s  }\n%*s}\n", indent, "", indent, "", indent, "");
+}
+
+/* ---- spatial collect ----
+ * The collect pass is order-independent: each primitive sets its own membership
+ * bit and adds its own events, and a primitive the ray does not reach keeps bit 0
+ * and adds none -- its true state.  So any grouping of the primitives may cull,
+ * not only the CSG tree's subtrees (BOUND records: a union cluster's hierarchy).
+ * For a tree without such structure (csg256 chain: a left-deep chain whose
+ * operands are scattered spheres) the primitives with a bounding sphere are
+ * grouped by a median-split hierarchy and tested against the wave's rays group by
+ * group; unbounded primitives (half-space-only convex primitives) are tested as
+ * before.  The root evaluation then reads the bits alone (a culled primitive's
+ * bits stay 0). */
+typedef struct SPrim {
+    double c[3], r;
+    uint32_t pc;
+} SPrim;
+
+/* a primitive's bounding sphere: its smallest sphere member (an intersection lies
+ * inside each member); 0 when it has none */
+static int prim_sphere(const WoRec* prog, uint32_t pc, SPrim* out) {
+    const uint32_t cnt = prog[pc].u0;
+    int found = 0;
+    for (uint32_t m = 0; m < cnt; ++m) {
+        const WoRec* L = &prog[pc + 1 + m];
+        if (L->op != WO_LEAF_SPHERE) continue;
+        const double r = sqrt((double)L->f[3]);
+        if (!found || r < out->r) {
+            out->c[0] = L->f[0], out->c[1] = L->f[1], out->c[2] = L->f[2], out->r = r;
+            found = 1;
+        }
+    }
+    out->pc = pc;
+    return found;
+}
+
+/* one comparator per axis (no shared state: scenes may be generated on several threads) */
+#define SPRIM_CMP(A)                                                          \
+    static int sprim_cmp##A(const void* a, const void* b) {                  \
+        const double x = ((const SPrim*)a)->c[A], y = ((const SPrim*)b)->c[A]; \
+        return x < y ? -1 : x > y;                                            \
+    }
+SPRIM_CMP(0)
+SPRIM_CMP(1)
+SPRIM_CMP(2)
+
+/* the enclosing sphere of p[0..n), expanded as the scene compiler expands BOUNDs */
+static void sprim_bound(const SPrim* p, uint32_t n, double c[3], double* R) {
+    double lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) lo[a] = hi[a] = p[0].c[a];
+    for (uint32_t i = 0; i < n; ++i)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fmin(lo[a], p[i].c[a] - p[i].r);
+            hi[a] = fmax(hi[a], p[i].c[a] + p[i].r);
+        }
+    for (int a = 0; a < 3; ++a) c[a] = 0.5 * (lo[a] + hi[a]);
+    double r = 0.0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const double dx = p[i].c[0] - c[0], dy = p[i].c[1] - c[1], dz = p[i].c[2] - c[2];
+        r = fmax(r, sqrt(dx * dx + dy * dy + dz * dz) + p[i].r);
+    }
+    const double cn = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    *R = r * (1.0 + 1e-4) + 1e-5 * (cn + r) + 1e-6;
+}
+
+/* groups tested by the hierarchy over p[0..n) (the root is not tested) */
+static uint32_t spatial_nodes(const Gen* g, uint32_t n, int root) {
+    if (n <= 1u) return 0;
+    const uint32_t self = root ? 0u : 1u;
+    if (n <= g->spatial_leaf) return self;
+    return self + spatial_nodes(g, n / 2u, 0) + spatial_nodes(g, n - n / 2u, 0);
+}
+
+static void gen_spatial(Gen* g, SPrim* p, uint32_t n, int indent, int root) {
+    if (n == 0u || g->err) return;
+    if (n == 1u) {
+        gen_collect(g, p[0].pc, p[0].pc + 1u + g->prog[p[0].pc].u0, indent);
+        return;
+    }
+    int inner = indent;
+    if (!root) {
+        double c[3], R;
+        sprim_bound(p, n, c, &R);
+        const uint32_t k = g->nbound++;
+        if (g->first_pass) {
+            const float fc[3] = {(float)c[0], (float)c[1], (float)c[2]};
+            const float fR = (float)R, fR2 = (float)(R * R);
+            uint32_t vr2 = fbits(fR2);
+            static const char* nr[1] = {"bc3"};
+            bput(g->b, "%*s{  // group %u (%u primitives)\n%*s  WO_WK(WO_WORK_BOUND_TESTS);\n", indent, "", k, n, indent,
+                 "");
+            emit_consts(g->b, indent + 2, "float", nr, &vr2, 1);
+            bput(g->b,
+                 "%*s  float ox, oy, oz, tca, d2, tr;\n"
+                 "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(ox) : \"v\"(o.x));\n"
+                 "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oy) : \"v\"(o.y));\n"
+                 "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oz) : \"v\"(o.z));\n"
+                 "%*s  wodev::bound_tca_d2(ox, oy, oz, d, tca, d2);\n"
+                 "%*s  asm(\"v_add_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(tr) : \"v\"(tca));\n"
+                 "%*s  const bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, bc3)) | (tr < 0.0f);\n"
+                 "%*s  if (__ballot(!miss) == 0ull) cull[%u] |= %uu;\n"
+                 "%*s}\n",
+                 indent, "", indent, "", fbits(fc[0]), indent, "", fbits(fc[1]), indent, "", fbits(fc[2]), indent, "",
+                 indent, "", fbits(fR), indent, "", indent, "", k / 32, 1u << (k % 32), indent, "");
+        }
+        bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
+        inner = indent + 2;
+    }
+    if (n <= g->spatial_leaf) {
+        for (uint32_t i = 0; i < n; ++i) gen_collect(g, p[i].pc, p[i].pc + 1u + g->prog[p[i].pc].u0, inner);
+    } else {
+        /* median split along the longest axis of the centres */
+        double lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) lo[a] = hi[a] = p[0].c[a];
+        for (uint32_t i = 0; i < n; ++i)
+            for (int a = 0; a < 3; ++a) lo[a] = fmin(lo[a], p[i].c[a]), hi[a] = fmax(hi[a], p[i].c[a]);
+        int ax = 0;
+        for (int a = 1; a < 3; ++a)
+            if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
+        qsort(p, n, sizeof(SPrim), ax == 0 ? sprim_cmp0 : ax == 1 ? sprim_cmp1 : sprim_cmp2);
+        gen_spatial(g, p, n / 2u, inner, 0);
+        gen_spatial(g, p + n / 2u, n - n / 2u, inner, 0);
+    }
+    if (!root) bput(g->b, "%*s}\n", indent, "");
+}
+
+/* the collect of the whole program in spatial groups: unbounded primitives
+ * first, in program order, then the hierarchy (same order in both passes) */
+static void gen_collect_spatial(Gen* g, const SPrim* bounded, uint32_t nb, int indent) {
+    for (uint32_t pc = 0; pc < g->n && !g->err;) {
+        const WoRec* r = &g->prog[pc];
+        if (r->op != WO_OP_PRIM) {
+            ++pc;
+            continue;
+        }
+        int grouped = 0;
+        for (uint32_t i = 0; i < nb && !grouped; ++i) grouped = bounded[i].pc == pc;
+        if (!grouped) gen_collect(g, pc, pc + 1u + r->u0, indent);
+        pc += 1u + r->u0;
+    }
+    if (!nb) return;
+    SPrim* p = (SPrim*)malloc(sizeof(SPrim) * nb);
+    if (!p) {
+        g->err = 1;
+        return;
+    }
+    memcpy(p, bounded, sizeof(SPrim) * nb); /* gen_spatial sorts in place: the same order each pass */
+    gen_spatial(g, p, nb, indent, 1);
+    free(p);
+}
+
+/* the collect of the whole program (either pass) */
+static void gen_collect_all(Gen* g, int indent) {
+    g->nbound = 0;
+    if (g->spatial)
+        gen_collect_spatial(g, g->sprims, g->nsprims, indent);
+    else
+        gen_collect(g, 0, g->n, indent);
 }
 
 /* ---- eval: value of the subtree [start, end) as named 0/1 temporaries ---- */
@@ -909,9 +1073,8 @@ static void gen_union_sweep(Gen* g, const UTerm* uterms, uint32_t n_uterms, uint
          "        WO_WK(WO_WORK_RECOLLECTS);\n"
          "        win.clear();\n"
          "        {\n");
-    g->nbound = 0;
     g->first_pass = 0;
-    gen_collect(g, 0, n_recs, 10);
+    gen_collect_all(g, 10);
     bput(b,
          "        }\n"
          "        if (!win.next(key)) return false;\n"
@@ -1035,6 +1198,55 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         const char* v = getenv("WOLOLO_JIT_BOUND_SINGLE");
         if (v && *v) g.bound_single = v[0] != '0';
     }
+    /* spatial collect: by default for deep trees (no union-cluster hierarchy to
+     * cull with); WOLOLO_JIT_SPATIAL=0|1 forces it */
+    g.spatial = !g.lds_events;
+    g.spatial_leaf = 8; /* csg256 chain: 15.04 / 13.93 / 13.63 ms at 2 / 4 / 8 */
+    {
+        const char* v = getenv("WOLOLO_JIT_SPATIAL");
+        if (v && *v) g.spatial = v[0] != '0';
+        v = getenv("WOLOLO_JIT_SPATIAL_LEAF");
+        if (v && *v) g.spatial_leaf = (uint32_t)strtoul(v, NULL, 10);
+        if (g.spatial_leaf < 1u) g.spatial_leaf = 1u;
+    }
+    SPrim* sprims = NULL;
+    if (g.spatial) {
+        sprims = (SPrim*)malloc(sizeof(SPrim) * (n_prims ? n_prims : 1u));
+        if (!sprims) g.err = 1;
+        for (uint32_t pc = 0; sprims && pc < n_recs;) {
+            if (prog[pc].op != WO_OP_PRIM) {
+                ++pc;
+                continue;
+            }
+            if (prim_sphere(prog, pc, &sprims[g.nsprims])) ++g.nsprims;
+            pc += 1u + prog[pc].u0;
+        }
+        /* outsized primitives (radius > 16x the median, e.g. a ground sphere) stay
+         * out of the hierarchy, as the scene compiler keeps them out of its BVHs:
+         * inside it they would make every group above them a sphere no ray misses */
+        if (g.nsprims > 2u) {
+            double* rs = (double*)malloc(sizeof(double) * g.nsprims);
+            if (!rs) {
+                g.err = 1;
+            } else {
+                for (uint32_t i = 0; i < g.nsprims; ++i) rs[i] = sprims[i].r;
+                for (uint32_t i = 1; i < g.nsprims; ++i) /* insertion sort: a few hundred at most */
+                    for (uint32_t j = i; j > 0 && rs[j - 1] > rs[j]; --j) {
+                        const double t = rs[j];
+                        rs[j] = rs[j - 1];
+                        rs[j - 1] = t;
+                    }
+                const double med = rs[g.nsprims / 2u];
+                free(rs);
+                uint32_t k = 0;
+                for (uint32_t i = 0; i < g.nsprims; ++i)
+                    if (!(sprims[i].r > 16.0 * med)) sprims[k++] = sprims[i];
+                g.nsprims = k;
+            }
+        }
+        g.sprims = sprims;
+        nbounds += spatial_nodes(&g, g.nsprims, 1);
+    }
     for (uint32_t i = 0; i < n_recs; ++i) nbounds += prog[i].op == WO_OP_BOUND && bound_tested(&g, i);
 
     bput(&b, "// generated by scene_jit.c: %u records, %u primitives, %u bounds\n", n_recs, n_prims, nbounds);
@@ -1131,9 +1343,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "    {\n",
              !g.lds_events ? "wodev::Window" : g.pair_window ? "wodev::PairLdsWindow" : "wodev::LdsWindow",
              !g.lds_events ? "" : g.pair_window ? "win.rest.ev = ev; " : "win.ev = ev; ");
-        g.nbound = 0;
         g.first_pass = 1;
-        gen_collect(&g, 0, n_recs, 6);
+        gen_collect_all(&g, 6);
         bput(&b,
              "    }\n"
              "    WO_MARK(\"collect_end\");\n"
@@ -1203,9 +1414,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  "        WO_WK(WO_WORK_RECOLLECTS);\n"
                  "        win.clear();\n"
                  "        {\n");
-            g.nbound = 0;
             g.first_pass = 0;
-            gen_collect(&g, 0, n_recs, 10);
+            gen_collect_all(&g, 10);
             bput(&b,
                  "        }\n"
                  "        if (!win.next(key)) return false;\n"
@@ -1275,6 +1485,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     if (eval_ops) bput(&b, "// wo_eval_ops_per_event %u\n", eval_ops);
     free(g.dls);
     free(uterms);
+    free(sprims);
     if (g.err || b.oom) {
         free(b.s);
         return NULL;

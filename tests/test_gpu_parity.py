@@ -462,6 +462,9 @@ def test_jit_event_windows(window, monkeypatch):
     {"WOLOLO_JIT_FLAGS": "-DWO_LDS_NEXT_EAGER=0"},
     {"WOLOLO_JIT_FLAGS": "-DWO_LDS_NEXT_EAGER=7"},
     {"WOLOLO_JIT_FLAGS": "-DWO_LDS_EVENTS=2 -DWO_LDS_NEXT_EAGER=7"},  # eager reads clamped to the list
+    {"WOLOLO_JIT_SPATIAL": "1"},  # spatial groups instead of the union clusters' bounds
+    {"WOLOLO_JIT_SPATIAL": "1", "WOLOLO_JIT_SPATIAL_LEAF": "1"},
+    {"WOLOLO_JIT_SPATIAL": "0", "WOLOLO_JIT_UNION_COUNT": "0", "WOLOLO_JIT_DL_EVAL": "0"},
 ])
 def test_jit_culling_knobs(knobs, monkeypatch):
     """The wave-level member skip, the bound-around-a-lone-primitive rule, the
