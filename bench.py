@@ -58,8 +58,10 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N>1: gather each frame before the next renders (default: frame k+1 renders while frame k "
                          "is gathered, with either backend)")
-    ap.add_argument("--frames-in-flight", type=int, default=1,
-                    help="render streams / buffers: frame k+1 may start while frame k's last tiles finish")
+    ap.add_argument("--frames-in-flight", type=int, default=None,
+                    help="render streams / buffers: frame k+1 may start while frame k's last tiles finish "
+                         "(default: 2 for pipelined N>1 runs, whose short per-rank launches lose their tails "
+                         "otherwise; 1 at N=1, where the per-launch HIP-event durations feed the roofline)")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 checks the assembled frame against a single full-frame render (bit-exact)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -110,6 +112,8 @@ def main():
     # the same two-buffer / two-stream / event code runs on either backend, so a gloo
     # rehearsal on one GPU executes what the RCCL run on 8 GPUs does
     pipelined = world > 1 and not args.no_pipeline
+    if args.frames_in_flight is None:
+        args.frames_in_flight = 2 if pipelined else 1
     # two render buffers when pipelined: frame k+1 renders while frame k is gathered; with F frames
     # in flight, F buffers and F render streams
     nbuf = max(args.frames_in_flight, 2 if pipelined else 1)
@@ -274,7 +278,8 @@ def main():
                        "scene": info.name, "width": W, "height": H, "spp": params.spp,
                        "max_depth": params.max_depth, "tile_rows": T,
                        "parallelism": f"row-cyclic tiles x{world}" + (f" + {'gloo (host-staged)' if gloo else 'RCCL'} gather" if world > 1 else "")
-                                      + (" overlapped with the next frame's render" if pipelined else "")},
+                                      + (" overlapped with the next frame's render" if pipelined else ""),
+                       "frames_in_flight": args.frames_in_flight},
             "fps": round(steps / elapsed_s, 3),
             "msamples_per_s": round(samples * steps / elapsed_s / 1e6, 3),
             "segments_per_frame": segs_all // steps,

@@ -26,12 +26,14 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("nranks", [2, 8])
-def test_pipelined_rehearsal_verifies(nranks):
+@pytest.mark.parametrize("nranks,fif", [(2, None), (8, None), (2, 1)])
+def test_pipelined_rehearsal_verifies(nranks, fif):
+    """N ranks, frames pipelined with the gather; by default two frames in flight on
+    two render streams (fif None), and with one render stream (fif 1)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(nranks),
            "--dist-backend", "gloo", "--verify", "--steps", "4", "--warmup", "1", "--no-cpu-baseline",
-           "--width", "480", "--height", "270", "--spp", "8"]
+           "--width", "480", "--height", "270", "--spp", "8"] + (["--frames-in-flight", str(fif)] if fif else [])
     env = dict(os.environ, OMP_NUM_THREADS="1")
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=150)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -41,5 +43,6 @@ def test_pipelined_rehearsal_verifies(nranks):
     assert line["n_gpus"] == nranks
     assert line["verified_vs_full_render"] is True
     assert "overlapped" in line["config"]["parallelism"]
+    assert line["config"]["frames_in_flight"] == (fif or 2)
     # every rank's segments are counted: the whole frame's
     assert line["segments_per_frame"] > 480 * 270 * 8
