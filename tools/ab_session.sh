@@ -1,13 +1,11 @@
 #!/usr/bin/env bash
-# Round-2 A/B session: spatial collect leaf size and event window on the chain.
+# Round-2 session: N>1 rehearsals (frames in flight), chain evidence with the spatial collect,
+# and per-rank shares with back-to-back frames on two streams.
 S=tools/gpu_session.sh
-B="python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-count-work"
 bash $S \
- "ch8:200:$B --scene csg256_chain > gpurun_out/ab_ch8.json" \
- "ch12:200:WOLOLO_JIT_SPATIAL_LEAF=12 $B --scene csg256_chain > gpurun_out/ab_ch12.json" \
- "ch16:200:WOLOLO_JIT_SPATIAL_LEAF=16 $B --scene csg256_chain > gpurun_out/ab_ch16.json" \
- "ch6:200:WOLOLO_JIT_SPATIAL_LEAF=6 $B --scene csg256_chain > gpurun_out/ab_ch6.json" \
- "ch8lds:200:WOLOLO_JIT_LDS_EVENTS=1 WOLOLO_JIT_SPATIAL=1 $B --scene csg256_chain > gpurun_out/ab_ch8lds.json" \
- "ch8w6:200:WOLOLO_JIT_FLAGS=-DWO_WINDOW=6 $B --scene csg256_chain > gpurun_out/ab_ch8w6.json" \
- "ch8w4:200:WOLOLO_JIT_FLAGS=-DWO_WINDOW=4 $B --scene csg256_chain > gpurun_out/ab_ch8w4.json" \
- "ch8b:200:$B --scene csg256_chain > gpurun_out/ab_ch8b.json"
+ "dist:400:python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 300 --timeout-method thread" \
+ "b256c:200:python bench.py --scene csg256_chain --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r02_bench_256c.json" \
+ "p256c:400:bash tools/profile_session.sh csg256c_jit --scene csg256_chain --steps 5 --warmup 1" \
+ "rs256c:300:python tools/rank_share.py --scene csg256_chain --worlds 1 8 --reps 3 > gpurun_out/r02_share256c.log 2>&1" \
+ "rs32s:300:python tools/rank_share.py --scene csg32 --worlds 8 --reps 3 --stream-frames 20 > gpurun_out/r02_share32_stream.log 2>&1" \
+ "par:500:python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k 'chain'"
