@@ -98,6 +98,7 @@ typedef struct Gen {
     int dl_eval;      /* chains of literal sets evaluated as decision lists (gen_eval_flat) */
     int union_count;  /* root a union of literal sets: a count of true terms kept per event */
     int spatial;      /* collect grouped by a spatial hierarchy over the primitives (gen_spatial) */
+    int spatial_sah;  /* its splits by least surface area instead of at the median */
     uint32_t spatial_leaf; /* most primitives in a leaf group of that hierarchy */
     struct SPrim* sprims;  /* the bounded primitives it groups */
     uint32_t nsprims;
@@ -388,13 +389,6 @@ static void sprim_bound(const SPrim* p, uint32_t n, double c[3], double* R) {
     *R = r * (1.0 + 1e-4) + 1e-5 * (cn + r) + 1e-6;
 }
 
-/* groups tested by the hierarchy over p[0..n) (the root is not tested) */
-static uint32_t spatial_nodes(const Gen* g, uint32_t n, int root) {
-    if (n <= 1u) return 0;
-    const uint32_t self = root ? 0u : 1u;
-    if (n <= g->spatial_leaf) return self;
-    return self + spatial_nodes(g, n / 2u, 0) + spatial_nodes(g, n - n / 2u, 0);
-}
 
 static void gen_spatial(Gen* g, SPrim* p, uint32_t n, int indent, int root) {
     if (n == 0u || g->err) return;
@@ -434,17 +428,34 @@ static void gen_spatial(Gen* g, SPrim* p, uint32_t n, int indent, int root) {
     if (n <= g->spatial_leaf) {
         for (uint32_t i = 0; i < n; ++i) gen_collect(g, p[i].pc, p[i].pc + 1u + g->prog[p[i].pc].u0, inner);
     } else {
-        /* median split along the longest axis of the centres */
-        double lo[3], hi[3];
-        for (int a = 0; a < 3; ++a) lo[a] = hi[a] = p[0].c[a];
-        for (uint32_t i = 0; i < n; ++i)
-            for (int a = 0; a < 3; ++a) lo[a] = fmin(lo[a], p[i].c[a]), hi[a] = fmax(hi[a], p[i].c[a]);
+        uint32_t cut = n / 2u;
         int ax = 0;
-        for (int a = 1; a < 3; ++a)
-            if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
+        if (g->spatial_sah) {
+            /* surface-area split: over the three axes (centres sorted) and every cut,
+             * the least R_left^2 * n_left + R_right^2 * n_right of the enclosing spheres */
+            double best = -1.0;
+            for (int a = 0; a < 3; ++a) {
+                qsort(p, n, sizeof(SPrim), a == 0 ? sprim_cmp0 : a == 1 ? sprim_cmp1 : sprim_cmp2);
+                for (uint32_t k = 1; k < n; ++k) {
+                    double cl[3], cr[3], rl, rr;
+                    sprim_bound(p, k, cl, &rl);
+                    sprim_bound(p + k, n - k, cr, &rr);
+                    const double cost = rl * rl * k + rr * rr * (n - k);
+                    if (best < 0.0 || cost < best) best = cost, ax = a, cut = k;
+                }
+            }
+        } else {
+            /* median split along the longest axis of the centres */
+            double lo[3], hi[3];
+            for (int a = 0; a < 3; ++a) lo[a] = hi[a] = p[0].c[a];
+            for (uint32_t i = 0; i < n; ++i)
+                for (int a = 0; a < 3; ++a) lo[a] = fmin(lo[a], p[i].c[a]), hi[a] = fmax(hi[a], p[i].c[a]);
+            for (int a = 1; a < 3; ++a)
+                if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
+        }
         qsort(p, n, sizeof(SPrim), ax == 0 ? sprim_cmp0 : ax == 1 ? sprim_cmp1 : sprim_cmp2);
-        gen_spatial(g, p, n / 2u, inner, 0);
-        gen_spatial(g, p + n / 2u, n - n / 2u, inner, 0);
+        gen_spatial(g, p, cut, inner, 0);
+        gen_spatial(g, p + cut, n - cut, inner, 0);
     }
     if (!root) bput(g->b, "%*s}\n", indent, "");
 }
@@ -1198,13 +1209,18 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         const char* v = getenv("WOLOLO_JIT_BOUND_SINGLE");
         if (v && *v) g.bound_single = v[0] != '0';
     }
-    /* spatial collect: by default for deep trees (no union-cluster hierarchy to
-     * cull with); WOLOLO_JIT_SPATIAL=0|1 forces it */
-    g.spatial = !g.lds_events;
-    g.spatial_leaf = 8; /* csg256 chain: 15.04 / 13.93 / 13.63 ms at 2 / 4 / 8 */
+    /* spatial collect (surface-area splits, leaves of <= 8): by default for deep
+     * trees (no union-cluster hierarchy to cull with: csg256 chain 18.40 -> 13.59 ms)
+     * and small scenes (csg32 3.716 -> 3.586 ms, 3840x2160x256 56.08 -> 54.45);
+     * csg256 balanced's SAH cluster hierarchy over its pairs culls better (10.10 vs
+     * 10.58 ms).  WOLOLO_JIT_SPATIAL=0|1 forces it either way. */
+    g.spatial = !g.lds_events || n_prims <= 64u;
+    g.spatial_leaf = 8; /* median splits, chain: 15.04 / 13.93 / 13.63 ms at 2 / 4 / 8; SAH, csg32: 3.687 / 3.612 / 3.628 / 3.589 at 3 / 4 / 6 / 8 */
     {
         const char* v = getenv("WOLOLO_JIT_SPATIAL");
         if (v && *v) g.spatial = v[0] != '0';
+        v = getenv("WOLOLO_JIT_SPATIAL_SAH");
+        g.spatial_sah = !(v && *v && v[0] == '0');
         v = getenv("WOLOLO_JIT_SPATIAL_LEAF");
         if (v && *v) g.spatial_leaf = (uint32_t)strtoul(v, NULL, 10);
         if (g.spatial_leaf < 1u) g.spatial_leaf = 1u;
@@ -1245,7 +1261,18 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             }
         }
         g.sprims = sprims;
-        nbounds += spatial_nodes(&g, g.nsprims, 1);
+        {
+            /* the groups it tests: a dry run of the emitter into a scratch buffer */
+            Buf scratch = {0};
+            Buf* keep = g.b;
+            g.b = &scratch;
+            g.nbound = 0;
+            g.first_pass = 1;
+            gen_collect_spatial(&g, g.sprims, g.nsprims, 0);
+            nbounds += g.nbound;
+            g.b = keep;
+            free(scratch.s);
+        }
     }
     for (uint32_t i = 0; i < n_recs; ++i) nbounds += prog[i].op == WO_OP_BOUND && bound_tested(&g, i);
 

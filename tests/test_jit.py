@@ -9,7 +9,10 @@ from csgrenderer_amd import scenes
 from csgrenderer_amd import wololo as wl
 
 
-def test_csg32_source_compiles_for_gfx950(hostonly):
+def test_csg32_source_compiles_for_gfx950(hostonly, monkeypatch):
+    # the scene compiler's BOUND records as the culling structure (WOLOLO_JIT_SPATIAL=0);
+    # the default spatial groups are checked at the end
+    monkeypatch.setenv("WOLOLO_JIT_SPATIAL", "0")
     r = wl.Renderer("jit", max_nodes=4096)
     scenes.build("csg32", r)
     prog, nrec, nprim = r.program()
@@ -43,6 +46,20 @@ def test_csg32_source_compiles_for_gfx950(hostonly):
     assert pcs == [i for i in range(nrec) if prog[i].op == wl.WO_OP_PRIM]
     log = wl.jit_compile_check(src, "gfx950")
     assert log == "", log
+    r.close()
+    # default for a small scene: the primitives grouped spatially (scene_jit.c gen_spatial),
+    # one wave-level test per group, no BOUND record tested; every leaf still intersected in both passes
+    monkeypatch.delenv("WOLOLO_JIT_SPATIAL")
+    r = wl.Renderer("jit", max_nodes=4096)
+    scenes.build("csg32", r)
+    src = r.jit_source()
+    ngroups = len(re.findall(r"// group \d+ \((\d+) primitives\)", src))  # the first pass tests them
+    assert ngroups >= 2 and "// BOUND" not in src
+    assert len(re.findall(r"if \(__ballot\(!miss\) == 0ull\)", src)) == ngroups
+    nsingle = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|sphere_need|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
+    npair = len(re.findall(r"wodev::axis_pair_meet(_d)?\(", src))
+    assert nsingle + 2 * npair == 2 * nleaf
+    assert wl.jit_compile_check(src, "gfx950") == ""
     r.close()
 
 

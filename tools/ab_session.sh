@@ -1,11 +1,15 @@
 #!/usr/bin/env bash
-# Round-2 session: N>1 rehearsals (frames in flight), chain evidence with the spatial collect,
-# and per-rank shares with back-to-back frames on two streams.
+# Round-2 A/B session: spatial collect (surface-area splits) on csg32.
 S=tools/gpu_session.sh
+B="python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-count-work"
 bash $S \
- "dist:400:python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 300 --timeout-method thread" \
- "b256c:200:python bench.py --scene csg256_chain --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r02_bench_256c.json" \
- "p256c:400:bash tools/profile_session.sh csg256c_jit --scene csg256_chain --steps 5 --warmup 1" \
- "rs256c:300:python tools/rank_share.py --scene csg256_chain --worlds 1 8 --reps 3 > gpurun_out/r02_share256c.log 2>&1" \
- "rs32s:300:python tools/rank_share.py --scene csg32 --worlds 8 --reps 3 --stream-frames 20 > gpurun_out/r02_share32_stream.log 2>&1" \
- "par:500:python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k 'chain'"
+ "c32:200:WOLOLO_JIT_SPATIAL=0 $B > gpurun_out/ab_c32.json" \
+ "c32_sp:200:WOLOLO_JIT_SPATIAL=1 $B > gpurun_out/ab_c32_sp.json" \
+ "c32_sp4:200:WOLOLO_JIT_SPATIAL=1 WOLOLO_JIT_SPATIAL_LEAF=4 $B > gpurun_out/ab_c32_sp4.json" \
+ "c32_sp6:200:WOLOLO_JIT_SPATIAL=1 WOLOLO_JIT_SPATIAL_LEAF=6 $B > gpurun_out/ab_c32_sp6.json" \
+ "c32_sp3:200:WOLOLO_JIT_SPATIAL=1 WOLOLO_JIT_SPATIAL_LEAF=3 $B > gpurun_out/ab_c32_sp3.json" \
+ "c32b:200:WOLOLO_JIT_SPATIAL=0 $B > gpurun_out/ab_c32b.json" \
+ "c32_spb:200:WOLOLO_JIT_SPATIAL=1 $B > gpurun_out/ab_c32_spb.json" \
+ "c4:300:WOLOLO_JIT_SPATIAL=0 python bench.py --width 3840 --height 2160 --spp 256 --steps 3 --warmup 1 --no-cpu-baseline --no-count-work > gpurun_out/ab_c4.json" \
+ "c4_sp:300:WOLOLO_JIT_SPATIAL=1 python bench.py --width 3840 --height 2160 --spp 256 --steps 3 --warmup 1 --no-cpu-baseline --no-count-work > gpurun_out/ab_c4_sp.json" \
+ "par:500:python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k 'knobs or chain'"
