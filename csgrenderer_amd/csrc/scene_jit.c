@@ -1097,7 +1097,7 @@ static void gen_union_sweep(Gen* g, const UTerm* uterms, uint32_t n_uterms, uint
          "      {\n"
          "        const uint32_t ord = ((uint32_t)key) >> 12;\n"
          "        const uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n"
-         "        const WoUTerm t = kUTerm[ord];\n");
+         "        const WoUTerm t = WO_UTERM[ord];\n");
     if (nw == 1u) {
         bput(b, "        const uint64_t cw = bits[0];\n");
     } else {
@@ -1326,6 +1326,19 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  (unsigned long long)u->q, u->w, u->neg);
         }
         bput(&b, "};\n");
+        /* the table in LDS (WOLOLO_JIT_LDS_UTERM=1): no gain for csg32 (3.614 / 3.583 ms
+         * against 3.581 / 3.597 from constant memory), csg256 balanced 10.01 -> 11.57 (LDS
+         * occupancy); off */
+        int lds_ut = 0;
+        {
+            const char* v = getenv("WOLOLO_JIT_LDS_UTERM");
+            if (v && *v) lds_ut = v[0] != '0';
+        }
+        if (lds_ut)
+            bput(&b, "__shared__ WoUTerm s_uterm[%u];\n#define WO_UTERM s_uterm\n#define WO_JIT_LDS_UTERM %u\n", n_prims,
+                 n_prims * 8u);
+        else
+            bput(&b, "#define WO_UTERM kUTerm\n");
     }
     bput(&b, "__constant__ uint32_t kOrdPc[%u] = {", n_prims ? n_prims : 1u);
     if (!n_prims) bput(&b, "0u");
@@ -1498,6 +1511,10 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "  tr.prog = prog;\n"
          "  tr.ordpc = kOrdPc;\n"
          "  const WoMaterial* m = mats;\n"
+         "#endif\n"
+         "#ifdef WO_JIT_LDS_UTERM  // the union count's term table (pathtrace_block's first barrier orders the copy)\n"
+         "  for (uint32_t i = threadIdx.x; i < WO_JIT_LDS_UTERM; i += wodev::kBlock)\n"
+         "    reinterpret_cast<uint32_t*>(s_uterm)[i] = reinterpret_cast<const uint32_t*>(kUTerm)[i];\n"
          "#endif\n"
          "#if WO_JIT_LDS_EVENTS && WO_SORT_RAYS\n"
          "  static_assert(wodev::kLdsEvents >= 6u, \"a ray's state fits the event list column\");\n"

@@ -304,7 +304,8 @@ def _compile_sweep(tmp_path, src, nw, ncull):
     m = re.search(r"struct __attribute__\(\(aligned\(16\)\)\) WoUTerm \{[^}]*\};", src)
     if m:
         t = re.search(r"__constant__ WoUTerm kUTerm\[\d+\] = \{.*?\};", src, re.S)
-        table = m.group(0) + "\n" + t.group(0).replace("__constant__", "static const") + "\n"
+        table = (m.group(0) + "\n" + t.group(0).replace("__constant__", "static const") + "\n"
+                 "#define WO_UTERM kUTerm\n")
         assert "ucnt" in toggle
     root_after = "(ucnt != 0)" if table else None
     c = tmp_path / "ev.cpp"
