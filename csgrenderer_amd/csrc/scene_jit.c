@@ -1134,8 +1134,10 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     /* Wave-level BOUND tests pay only for larger subtrees (measured: csg32 6.54 ms
      * testing subtrees of >= 8 leaves vs 6.94 ms testing every BOUND record; with
      * the later kernel 5.17 ms at >= 8, 5.11 at >= 6, 5.13 at >= 5, 5.30 at >= 12; with fused slab
-     * faces 4.93 at >= 6, 4.95 at 4 / 5, 4.98 at 7, 4.99 at 8; csg256 balanced 15.0 at 6, 15.2 at 4 / 8). */
-    g.bound_min_leaves = 6;
+     * faces 4.93 at >= 6, 4.95 at 4 / 5, 4.98 at 7, 4.99 at 8; csg256 balanced 15.0 at 6, 15.2 at 4 / 8).
+     * Round 2, with the union count (csg32 now takes the spatial collect): csg256 balanced
+     * 10.02 / 10.02 at 6, 9.84 / 9.80 at 4, 9.82 at 3, 10.00 at 5, 10.46 at 8. */
+    g.bound_min_leaves = 4;
     {
         const char* v = getenv("WOLOLO_JIT_BOUND_MIN_LEAVES");
         if (v && *v) g.bound_min_leaves = (uint32_t)strtoul(v, NULL, 10);

@@ -32,12 +32,12 @@ def test_csg32_source_compiles_for_gfx950(hostonly, monkeypatch):
     naxis = sum(1 for i in range(nrec) if prog[i].op == wl.WO_LEAF_HALFSPACE and prog[i].u1 != 0)
     assert naxis >= 12
     assert len(re.findall(r"wodev::halfspace_axis_(interval|dist)\(", src)) + 2 * npair == 2 * naxis
-    # wave-level tests only for BOUND subtrees of >= 6 leaves (scene_jit.c, WOLOLO_JIT_BOUND_MIN_LEAVES)
+    # wave-level tests only for BOUND subtrees of >= 4 leaves (scene_jit.c, WOLOLO_JIT_BOUND_MIN_LEAVES)
     # and not around a lone primitive (WOLOLO_JIT_BOUND_SINGLE=0: its member skip is the cheaper test)
     def lone(i):
         return prog[i + 1].op == wl.WO_OP_PRIM and i + 2 + prog[i + 1].u0 == prog[i].u0
 
-    nb = sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND and prog[i].u1 >= 6 and not lone(i))
+    nb = sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND and prog[i].u1 >= 4 and not lone(i))
     assert 0 < nb < sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND)
     assert len(re.findall(r"if \(__ballot\((wodev::bound_may_hit\(|!miss\) == 0ull)", src)) == nb
     m = re.search(r"kOrdPc\[(\d+)\] = \{([^}]*)\}", src)
