@@ -1,13 +1,9 @@
 #!/usr/bin/env bash
-# Round-2 A/B session: leaf children intersected at their parent in the lane walk
-# (abtest/inl: -DWO_LANES_INLINE_LEAF=1).
+# Round-2 final session: full GPU suite, smoke, csg256 balanced evidence (BOUNDs from 4 leaves).
 S=tools/gpu_session.sh
-B="python bench.py --scene rtiow_cover --steps 10 --warmup 2 --no-cpu-baseline --no-count-work"
-P=abtest/inl/libwololo.so
 bash $S \
- "rt:200:$B > gpurun_out/ab_rt.json" \
- "rt_i:200:WOLOLO_LIB=$P $B > gpurun_out/ab_rt_i.json" \
- "rtb:200:$B > gpurun_out/ab_rtb.json" \
- "rt_ib:200:WOLOLO_LIB=$P $B > gpurun_out/ab_rt_ib.json" \
- "rt_ic:200:WOLOLO_LIB=$P python bench.py --scene rtiow_cover --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/ab_rt_ic.json" \
- "par:500:WOLOLO_LIB=$P python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k 'lanes or rtiow'"
+ "gt:700:python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
+ "smoke:300:python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" \
+ "b256b:200:python bench.py --scene csg256_balanced --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r02_bench_256b.json" \
+ "p256b:400:bash tools/profile_session.sh csg256b_jit --scene csg256_balanced --steps 5 --warmup 1" \
+ "rs256b:300:python tools/rank_share.py --scene csg256_balanced --worlds 1 8 --reps 3 > gpurun_out/r02_share256b.log 2>&1"
