@@ -1,5 +1,6 @@
 """Scene-specialised kernels (csrc/scene_jit.c): the generated HIP source compiles
 for gfx950 with hiprtc (no GPU needed) and mirrors the compiled program (CPU)."""
+import math
 import re
 
 import numpy as np
@@ -380,3 +381,60 @@ def test_generated_root_evaluation(hostonly, monkeypatch, tmp_path, case, knobs)
         want = _program_value(prog, nrec, pack(cur))
         got = out[:, e].astype(bool)
         assert np.array_equal(got, want), (e, int(np.count_nonzero(got != want)))
+
+
+def _f32(h):
+    return float(np.array([int(h, 16)], dtype=np.uint32).view(np.float32)[0])
+
+
+@pytest.mark.parametrize("case", ["csg32", "csg256_chain", "unionpairs", "random_b"])
+def test_spatial_groups_enclose_their_primitives(hostonly, monkeypatch, case):
+    """Spatial collect (scene_jit.c gen_spatial): each wave-level group test's sphere
+    (centre and R, R^2 as emitted) encloses the bounding sphere of every primitive the
+    group skips when culled, so a culled group never hides a primitive a ray meets;
+    and every primitive is collected exactly once per pass."""
+    monkeypatch.setenv("WOLOLO_JIT_SPATIAL", "1")
+    r = wl.Renderer("sp", max_nodes=4096)
+    _build_case(r, case)
+    prog, nrec, nprim = r.program()
+    src = r.jit_source()
+    r.close()
+    # each primitive's bounding sphere: its smallest sphere member
+    pc_of = {prog[i].u1: i for i in range(nrec) if prog[i].op == wl.WO_OP_PRIM}
+    sph = {}
+    for o, pc in pc_of.items():
+        best = None
+        for m in range(prog[pc].u0):
+            L = prog[pc + 1 + m]
+            if L.op == wl.WO_LEAF_SPHERE:
+                rr = math.sqrt(L.f[3])
+                if best is None or rr < best[3]:
+                    best = (L.f[0], L.f[1], L.f[2], rr)
+        if best:
+            sph[o] = best
+    lines = src.splitlines()
+    first_pass = lines[:next(i for i, l in enumerate(lines) if "WO_MARK(\"collect_end\")" in l)]
+    groups = 0
+    for i, l in enumerate(first_pass):
+        m = re.search(r"// group (\d+) \((\d+) primitives\)", l)
+        if not m:
+            continue
+        groups += 1
+        lits = re.findall(r"0x([0-9a-f]{8})", "\n".join(first_pass[i:i + 12]))
+        r2, cx, cy, cz, rad = (_f32(x) for x in lits[:5])
+        # the guarded body: from the `if (!(cull...)) {` after the test block to its closing brace
+        j = next(k for k in range(i, len(first_pass)) if first_pass[k].strip().startswith("if (!(cull["))
+        ind = len(first_pass[j]) - len(first_pass[j].lstrip())
+        k = j + 1
+        while not (first_pass[k].strip() == "}" and len(first_pass[k]) - len(first_pass[k].lstrip()) == ind):
+            k += 1
+        ords = [int(x) for x in re.findall(r"// primitive (\d+) ", "\n".join(first_pass[j:k]))]
+        assert len(ords) == int(m.group(2))
+        for o in ords:
+            c = sph[o]
+            need = math.dist(c[:3], (cx, cy, cz)) + c[3]
+            assert need <= rad and need * need <= r2 * (1 + 1e-6), (case, m.group(1), o, need, rad)
+    assert groups >= 1
+    # every primitive once in the first pass and once in the re-collect pass
+    ords_all = [int(x) for x in re.findall(r"// primitive (\d+) ", src)]
+    assert sorted(ords_all) == sorted(list(range(nprim)) * 2)
