@@ -100,6 +100,7 @@ typedef struct Gen {
     int spatial;      /* collect grouped by a spatial hierarchy over the primitives (gen_spatial) */
     int spatial_sah;  /* its splits by least surface area instead of at the median */
     uint32_t spatial_leaf; /* most primitives in a leaf group of that hierarchy */
+    double spatial_ct;     /* group-test cost for SAH leaf decisions (0: split down to spatial_leaf) */
     struct SPrim* sprims;  /* the bounded primitives it groups */
     uint32_t nsprims;
     struct DList* dls; /* decision-list pool (ids are 1-based; 0 = none) */
@@ -425,7 +426,27 @@ static void gen_spatial(Gen* g, SPrim* p, uint32_t n, int indent, int root) {
         bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
         inner = indent + 2;
     }
-    if (n <= g->spatial_leaf) {
+    /* with a group-test cost (WOLOLO_JIT_SPATIAL_CT = c > 0), a set of up to twice the
+     * leaf size stays one group unless the best split's expected cost, c + (R_l^2 n_l +
+     * R_r^2 n_r) / R^2 primitive tests, is below the n tests of a leaf */
+    int leaf = n <= g->spatial_leaf;
+    if (!leaf && g->spatial_ct > 0.0 && g->spatial_sah && n <= 2u * g->spatial_leaf) {
+        double c[3], R;
+        sprim_bound(p, n, c, &R);
+        double best = -1.0;
+        for (int a = 0; a < 3; ++a) {
+            qsort(p, n, sizeof(SPrim), a == 0 ? sprim_cmp0 : a == 1 ? sprim_cmp1 : sprim_cmp2);
+            for (uint32_t k = 1; k < n; ++k) {
+                double cl[3], cr[3], rl, rr;
+                sprim_bound(p, k, cl, &rl);
+                sprim_bound(p + k, n - k, cr, &rr);
+                const double cost = rl * rl * k + rr * rr * (n - k);
+                if (best < 0.0 || cost < best) best = cost;
+            }
+        }
+        leaf = g->spatial_ct + best / (R * R) >= (double)n;
+    }
+    if (leaf) {
         for (uint32_t i = 0; i < n; ++i) gen_collect(g, p[i].pc, p[i].pc + 1u + g->prog[p[i].pc].u0, inner);
     } else {
         uint32_t cut = n / 2u;
@@ -1223,6 +1244,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         if (v && *v) g.spatial = v[0] != '0';
         v = getenv("WOLOLO_JIT_SPATIAL_SAH");
         g.spatial_sah = !(v && *v && v[0] == '0');
+        v = getenv("WOLOLO_JIT_SPATIAL_CT");
+        g.spatial_ct = v && *v ? strtod(v, NULL) : 0.0;
         v = getenv("WOLOLO_JIT_SPATIAL_LEAF");
         if (v && *v) g.spatial_leaf = (uint32_t)strtoul(v, NULL, 10);
         if (g.spatial_leaf < 1u) g.spatial_leaf = 1u;
