@@ -338,9 +338,12 @@ static void gen_lone_sphere(Gen* g, const WoRec* L, uint32_t ord, int indent) {
  * group; unbounded primitives (half-space-only convex primitives) are tested as
  * before.  The root evaluation then reads the bits alone (a culled primitive's
  * bits stay 0). */
+#define SUNIT_MAX 8
 typedef struct SPrim {
     double c[3], r;
-    uint32_t pc;
+    uint32_t pc;               /* a primitive's program counter ... */
+    uint32_t npc;              /* ... or, for a unit of several primitives (npc > 0), theirs */
+    uint32_t pcs[SUNIT_MAX];
 } SPrim;
 
 /* a primitive's bounding sphere: its smallest sphere member (an intersection lies
@@ -358,6 +361,7 @@ static int prim_sphere(const WoRec* prog, uint32_t pc, SPrim* out) {
         }
     }
     out->pc = pc;
+    out->npc = 0;
     return found;
 }
 
@@ -391,10 +395,18 @@ static void sprim_bound(const SPrim* p, uint32_t n, double c[3], double* R) {
 }
 
 
+static void gen_sprim(Gen* g, const SPrim* q, int indent) {
+    if (!q->npc) {
+        gen_collect(g, q->pc, q->pc + 1u + g->prog[q->pc].u0, indent);
+        return;
+    }
+    for (uint32_t k = 0; k < q->npc; ++k) gen_collect(g, q->pcs[k], q->pcs[k] + 1u + g->prog[q->pcs[k]].u0, indent);
+}
+
 static void gen_spatial(Gen* g, SPrim* p, uint32_t n, int indent, int root) {
     if (n == 0u || g->err) return;
     if (n == 1u) {
-        gen_collect(g, p[0].pc, p[0].pc + 1u + g->prog[p[0].pc].u0, indent);
+        gen_sprim(g, &p[0], indent);
         return;
     }
     int inner = indent;
@@ -407,8 +419,10 @@ static void gen_spatial(Gen* g, SPrim* p, uint32_t n, int indent, int root) {
             const float fR = (float)R, fR2 = (float)(R * R);
             uint32_t vr2 = fbits(fR2);
             static const char* nr[1] = {"bc3"};
-            bput(g->b, "%*s{  // group %u (%u primitives)\n%*s  WO_WK(WO_WORK_BOUND_TESTS);\n", indent, "", k, n, indent,
-                 "");
+            uint32_t nprim = 0;
+            for (uint32_t i = 0; i < n; ++i) nprim += p[i].npc ? p[i].npc : 1u;
+            bput(g->b, "%*s{  // group %u (%u primitives)\n%*s  WO_WK(WO_WORK_BOUND_TESTS);\n", indent, "", k, nprim,
+                 indent, "");
             emit_consts(g->b, indent + 2, "float", nr, &vr2, 1);
             bput(g->b,
                  "%*s  float ox, oy, oz, tca, d2, tr;\n"
@@ -447,7 +461,7 @@ static void gen_spatial(Gen* g, SPrim* p, uint32_t n, int indent, int root) {
         leaf = g->spatial_ct + best / (R * R) >= (double)n;
     }
     if (leaf) {
-        for (uint32_t i = 0; i < n; ++i) gen_collect(g, p[i].pc, p[i].pc + 1u + g->prog[p[i].pc].u0, inner);
+        for (uint32_t i = 0; i < n; ++i) gen_sprim(g, &p[i], inner);
     } else {
         uint32_t cut = n / 2u;
         int ax = 0;
@@ -491,7 +505,10 @@ static void gen_collect_spatial(Gen* g, const SPrim* bounded, uint32_t nb, int i
             continue;
         }
         int grouped = 0;
-        for (uint32_t i = 0; i < nb && !grouped; ++i) grouped = bounded[i].pc == pc;
+        for (uint32_t i = 0; i < nb && !grouped; ++i) {
+            if (!bounded[i].npc) grouped = bounded[i].pc == pc;
+            for (uint32_t k = 0; k < bounded[i].npc && !grouped; ++k) grouped = bounded[i].pcs[k] == pc;
+        }
         if (!grouped) gen_collect(g, pc, pc + 1u + r->u0, indent);
         pc += 1u + r->u0;
     }
@@ -1261,6 +1278,67 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             }
             if (prim_sphere(prog, pc, &sprims[g.nsprims])) ++g.nsprims;
             pc += 1u + prog[pc].u0;
+        }
+        /* WOLOLO_JIT_SPATIAL_UNITS=1: when the root is a union of literal-set terms, a
+         * term's primitives stay together as one unit of the hierarchy, bounded as the
+         * term's value is: a conjunction lies inside each of its positive literals (the
+         * smallest one's sphere: a pair a - b is bounded by a, and b is skipped with it,
+         * which is exact -- b only matters inside a), a disjunction inside the sphere
+         * around all of its primitives */
+        const char* uv = getenv("WOLOLO_JIT_SPATIAL_UNITS");
+        if (sprims && uv && uv[0] == '1' && n_prims) {
+            UTerm* ut = (UTerm*)malloc(sizeof(UTerm) * n_prims);
+            uint32_t* pc_of = (uint32_t*)malloc(sizeof(uint32_t) * n_prims);
+            const uint32_t nt = ut && pc_of ? union_terms(prog, n_recs, n_prims, ut, n_prims) : 0u;
+            if (nt && pc_of) {
+                for (uint32_t pc = 0; pc < n_recs;) {
+                    if (prog[pc].op != WO_OP_PRIM) {
+                        ++pc;
+                        continue;
+                    }
+                    pc_of[prog[pc].u1] = pc;
+                    pc += 1u + prog[pc].u0;
+                }
+                for (uint32_t i = 0; i < nt; ++i) {
+                    if (__builtin_popcountll(ut[i].m) < 2 || __builtin_popcountll(ut[i].m) > SUNIT_MAX) continue;
+                    SPrim u, parts[SUNIT_MAX], pos;
+                    memset(&pos, 0, sizeof pos);
+                    memset(&u, 0, sizeof u);
+                    int ok = 1, have_pos = 0;
+                    for (uint32_t bit = 0; bit < 64u && ok; ++bit) {
+                        if (!((ut[i].m >> bit) & 1u)) continue;
+                        const uint32_t o = 32u * ut[i].w + bit;
+                        ok = o < n_prims;
+                        if (!ok) break;
+                        const uint32_t pc = pc_of[o];
+                        const int bnd = prim_sphere(prog, pc, &parts[u.npc]);
+                        if (!ut[i].neg && ((ut[i].q >> bit) & 1u)) { /* a positive literal of a conjunction */
+                            if (bnd && (!have_pos || parts[u.npc].r < pos.r)) pos = parts[u.npc], have_pos = 1;
+                        } else if (ut[i].neg) {
+                            ok = bnd; /* a disjunction needs every member bounded */
+                        }
+                        u.pcs[u.npc++] = pc;
+                    }
+                    if (!ok || (!ut[i].neg && !have_pos)) continue; /* stays as single primitives */
+                    if (ut[i].neg) {
+                        sprim_bound(parts, u.npc, u.c, &u.r);
+                    } else {
+                        u.c[0] = pos.c[0], u.c[1] = pos.c[1], u.c[2] = pos.c[2], u.r = pos.r;
+                    }
+                    u.pc = u.pcs[0];
+                    /* the unit replaces its primitives (bounded ones in the single list, the
+                     * unbounded ones in the ungrouped list: gen_collect_spatial checks units) */
+                    for (uint32_t k = 0; k < u.npc; ++k)
+                        for (uint32_t j = 0; j < g.nsprims; ++j)
+                            if (!sprims[j].npc && sprims[j].pc == u.pcs[k]) {
+                                sprims[j] = sprims[--g.nsprims];
+                                break;
+                            }
+                    sprims[g.nsprims++] = u;
+                }
+            }
+            free(ut);
+            free(pc_of);
         }
         /* outsized primitives (radius > 16x the median, e.g. a ground sphere) stay
          * out of the hierarchy, as the scene compiler keeps them out of its BVHs:
