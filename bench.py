@@ -10,6 +10,14 @@ a HIP kernel.  A step = one full frame including the gather.
 
     python bench.py                       # N=1, defaults finish in about a minute
     torchrun --nproc-per-node 8 bench.py --gpus 8
+    python bench.py --gpus 8              # the same: starts torch.distributed.run itself
+    python bench.py --gpus 8 --single-process
+                                          # one process over 8 GPUs through the C API
+                                          # (wo_renderer_set_devices, peer-DMA gather)
+
+--gpus N must match the ranks that actually run: under a launcher WORLD_SIZE must
+equal N, and N ranks on the RCCL backend need N visible GPUs; anything else exits
+with status 2 (--stack-ranks allows more ranks than GPUs, for rehearsals only).
 
 Prints ONE JSON line on rank 0.  `value` = traced ray segments of the whole frame
 (all ranks) / max-over-ranks wall time of the timed steps.
@@ -20,6 +28,8 @@ import argparse
 import json
 import os
 import re
+import socket
+import subprocess
 import sys
 import time
 
@@ -38,7 +48,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scene", default="csg32",
-                    choices=["csg32", "rtiow_cover", "csg256_balanced", "csg256_chain", "csg32_union", "csg256_balanced_union",
+                    choices=["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain", "csg32_union", "csg256_balanced_union",
                              "sphere256"])
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
@@ -62,6 +72,12 @@ def parse():
                     help="render streams / buffers: frame k+1 may start while frame k's last tiles finish "
                          "(default: 2 for pipelined N>1 runs, whose short per-rank launches lose their tails "
                          "otherwise; 1 at N=1, where the per-launch HIP-event durations feed the roofline)")
+    ap.add_argument("--single-process", action="store_true",
+                    help="one process drives all N GPUs through the C API (wo_renderer_set_devices: each rank on its "
+                         "own device and stream, peer-DMA gather into rank 0, assembled there); a step is "
+                         "wo_renderer_render_frame_device")
+    ap.add_argument("--stack-ranks", action="store_true",
+                    help="allow more ranks than visible GPUs (ranks share devices): rehearsal only, the line says so")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 checks the assembled frame against a single full-frame render (bit-exact)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -69,17 +85,63 @@ def parse():
     return ap.parse_args()
 
 
+def fail(msg: str, code: int = 2):
+    print(f"[bench] error: {msg}", file=sys.stderr, flush=True)
+    sys.exit(code)
+
+
+def visible_devices() -> int:
+    # counting devices does not initialise HIP on this image (no GPU context yet)
+    import torch
+    return torch.cuda.device_count()
+
+
+def self_launch(args) -> int:
+    """`bench.py --gpus N` without a launcher: run N ranks under torch.distributed.run
+    as a child process (nothing here has touched the GPU) and return its status."""
+    ndev = visible_devices()
+    if ndev < args.gpus and not args.stack_ranks:
+        fail(f"--gpus {args.gpus} needs {args.gpus} GPUs, {ndev} visible (use --stack-ranks to rehearse "
+             f"{args.gpus} ranks on fewer, with --dist-backend gloo)")
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] no launcher: starting {args.gpus} ranks with torch.distributed.run", file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse()
+    if os.environ.get("WOLOLO_LOAD_FIRST") == "1":
+        # libwololo (and with it the ROCm installation's HIP runtime, hiprtc and comgr)
+        # before torch, whose wheel bundles its own: torch then shares the ones loaded
+        # here, and the specialised kernels compile with this image's ROCm
+        from csgrenderer_amd import wololo as _wl
+        _wl.load()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.single_process:
+        if world_env not in (None, "1"):
+            fail(f"--single-process drives every GPU from one process; WORLD_SIZE={world_env}")
+        return single_process(args)
+    if world_env is None and args.gpus > 1:
+        sys.exit(self_launch(args))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        fail(f"--gpus {args.gpus} but {world} ranks are running (WORLD_SIZE)")
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     ndev = torch.cuda.device_count()
+    if ndev < world and not args.stack_ranks:
+        fail(f"{world} ranks need {world} GPUs, {ndev} visible (--stack-ranks with --dist-backend gloo "
+             f"rehearses them on fewer)")
+    if ndev < world and args.dist_backend == "nccl":
+        fail("RCCL cannot put two ranks on one GPU: stacked ranks need --dist-backend gloo")
+    stacked = ndev < world
     dev_index = local_rank % max(ndev, 1)
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
@@ -216,78 +278,13 @@ def main():
         verified_all = verified is not False
 
     if rank == 0:
-        steps = args.steps
-        ms_per_step = elapsed_s / steps * 1e3
-        samples = W * H * (params.spp if info.mode == wl.MODE_PATHTRACE else 1)
-        if info.mode == wl.MODE_PATHTRACE:
-            value = segs_all / elapsed_s / 1e6
-            seg_launch = segs_local / steps
-            brute_tf = seg_launch * info.flop_per_segment / (k_ms * 1e-3) / 1e12
-            roof = {"bound": "valu", "achieved": None, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": None,
-                    "traffic": None,
-                    "kernel": {"jit": "wo_jit_pathtrace", "lanes": "pathtrace_lanes_kernel"}.get(r.trace_path(),
-                                                                                              "pathtrace_kernel"),
-                    "kernel_ms": round(k_ms, 4), "segments_per_launch": segs_local // steps,
-                    "trace_path": r.trace_path(),
-                    "brute_force_flop_per_segment": info.flop_per_segment,
-                    "brute_force_achieved": round(brute_tf, 3),
-                    "brute_force_frac": round(brute_tf / PEAK_FP32_TFLOPS, 4)}
-            if work is not None:
-                eval_ops = None
-                if r.trace_path() == "jit":
-                    m = re.search(r"// wo_eval_ops_per_event (\d+)", r.jit_source() or "")
-                    eval_ops = int(m.group(1)) if m else None
-                ex = executed_flop(work, info, r.trace_path(), eval_ops)
-                ex_tf = ex / work["segments"] * seg_launch / (k_ms * 1e-3) / 1e12
-                roof.update({"achieved": round(ex_tf, 3), "frac": round(ex_tf / PEAK_FP32_TFLOPS, 4),
-                             "basis": "executed work (counted tests priced per SURVEY.md 8(d); a swept event "
-                                      "priced at the emitted root evaluation's operations"
-                                      + (f", {eval_ops} per event)" if eval_ops else ")"),
-                             "executed_flop_per_segment": round(ex / work["segments"], 2),
-                             "work_per_segment": {k: round(v / work["segments"], 4) for k, v in work.items()
-                                                  if k != "segments" and not k.startswith("cyc_")}})
-            else:
-                roof.update({"achieved": roof["brute_force_achieved"], "frac": roof["brute_force_frac"],
-                             "basis": "brute force (every primitive on every segment, SURVEY.md 8(d))"})
-        else:
-            value = W * H * steps / elapsed_s / 1e6
-            bytes_launch = lr * W * 16
-            achieved = bytes_launch / (k_ms * 1e-3) / 1e9
-            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": None, "kernel": "ubershader_kernel",
-                    "kernel_ms": round(k_ms, 5)}
-        # the store stream (16 B/pixel) against HBM, for the record
-        hbm_gbs = lr * W * 16 / (k_ms * 1e-3) / 1e9
-        if args.pmc_json and os.path.exists(args.pmc_json):
-            try:
-                pmc = json.load(open(args.pmc_json))
-                key = f"{args.scene}:{W}x{H}:{params.spp}:{world}:{roof.get('trace_path', 'ubershader')}"
-                if key in pmc:
-                    roof["traffic"] = pmc[key]
-            except Exception as e:  # report, don't fail the bench
-                print(f"[bench] pmc json unreadable: {e}", file=sys.stderr)
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline and info.mode == wl.MODE_PATHTRACE:
-            cpu = cpu_baseline(r, params, args.cpu_seconds)
-        line = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"{info.name}: {W}x{H}, {params.spp} spp, {params.max_depth} bounces, "
-                                   f"{info.spheres} spheres + {info.halfspaces} half-spaces, {info.binops} binops",
-                       "scene": info.name, "width": W, "height": H, "spp": params.spp,
-                       "max_depth": params.max_depth, "tile_rows": T,
-                       "parallelism": f"row-cyclic tiles x{world}" + (f" + {'gloo (host-staged)' if gloo else 'RCCL'} gather" if world > 1 else "")
-                                      + (" overlapped with the next frame's render" if pipelined else ""),
-                       "frames_in_flight": args.frames_in_flight},
-            "fps": round(steps / elapsed_s, 3),
-            "msamples_per_s": round(samples * steps / elapsed_s / 1e6, 3),
-            "segments_per_frame": segs_all // steps,
-            "roofline": roof,
-            "roofline_hbm_store": {"bound": "hbm", "achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS,
-                                   "unit": "GB/s", "frac": round(hbm_gbs / PEAK_HBM_GBS, 6)},
-            "cpu_baseline": cpu,
-        }
+        parallelism = (f"row-cyclic tiles x{world}" + (f" + {'gloo (host-staged)' if gloo else 'RCCL'} gather" if world > 1 else "")
+                       + (" overlapped with the next frame's render" if pipelined else "")
+                       + (f"; {world} ranks stacked on {ndev} GPU(s) (rehearsal)" if stacked else ""))
+        line = report_line(args, r, info, params, world, elapsed_s, segs_all, segs_local, k_ms, work,
+                           {"parallelism": parallelism, "ranks": world, "devices": min(world, ndev),
+                            "launcher": "torchrun" if world_env else "none",
+                            "frames_in_flight": args.frames_in_flight})
         if verified is not None:
             line["verified_vs_full_render"] = verified
         print(json.dumps(line), flush=True)
@@ -295,6 +292,176 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     if not verified_all:
+        sys.exit(3)
+
+
+def report_line(args, r, info, params, world, elapsed_s, segs_all, segs_local, k_ms, work, cfg_extra):
+    """The JSON line (rank 0): value = segments of the whole frame over the max-over-ranks
+    wall time; roofline of the dominant kernel from its per-launch time k_ms and the
+    segments one launch traced (segs_local over the steps)."""
+    from csgrenderer_amd import wololo as wl
+    W, H, T = params.width, params.height, args.tile_rows
+    lr = wl.local_rows(H, T, world)
+    steps = args.steps
+    ms_per_step = elapsed_s / steps * 1e3
+    samples = W * H * (params.spp if info.mode == wl.MODE_PATHTRACE else 1)
+    if info.mode == wl.MODE_PATHTRACE:
+        value = segs_all / elapsed_s / 1e6
+        seg_launch = segs_local / steps
+        brute_tf = seg_launch * info.flop_per_segment / (k_ms * 1e-3) / 1e12
+        roof = {"bound": "valu", "achieved": None, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": None,
+                "traffic": None,
+                "kernel": {"jit": "wo_jit_pathtrace", "lanes": "pathtrace_lanes_kernel"}.get(r.trace_path(),
+                                                                                          "pathtrace_kernel"),
+                "kernel_ms": round(k_ms, 4), "segments_per_launch": segs_local // steps,
+                "trace_path": r.trace_path(),
+                "brute_force_flop_per_segment": info.flop_per_segment,
+                "brute_force_achieved": round(brute_tf, 3),
+                "brute_force_frac": round(brute_tf / PEAK_FP32_TFLOPS, 4)}
+        if work is not None:
+            eval_ops = None
+            if r.trace_path() == "jit":
+                m = re.search(r"// wo_eval_ops_per_event (\d+)", r.jit_source() or "")
+                eval_ops = int(m.group(1)) if m else None
+            ex = executed_flop(work, info, r.trace_path(), eval_ops)
+            ex_tf = ex / work["segments"] * seg_launch / (k_ms * 1e-3) / 1e12
+            roof.update({"achieved": round(ex_tf, 3), "frac": round(ex_tf / PEAK_FP32_TFLOPS, 4),
+                         "basis": "executed work (counted tests priced per SURVEY.md 8(d); a swept event "
+                                  "priced at the emitted root evaluation's operations"
+                                  + (f", {eval_ops} per event)" if eval_ops else ")"),
+                         "executed_flop_per_segment": round(ex / work["segments"], 2),
+                         "work_per_segment": {k: round(v / work["segments"], 4) for k, v in work.items()
+                                              if k != "segments" and not k.startswith("cyc_")}})
+        else:
+            roof.update({"achieved": roof["brute_force_achieved"], "frac": roof["brute_force_frac"],
+                         "basis": "brute force (every primitive on every segment, SURVEY.md 8(d))"})
+    else:
+        value = W * H * steps / elapsed_s / 1e6
+        bytes_launch = lr * W * 16
+        achieved = bytes_launch / (k_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": None, "kernel": "ubershader_kernel",
+                "kernel_ms": round(k_ms, 5)}
+    # the store stream (16 B/pixel) against HBM, for the record
+    hbm_gbs = lr * W * 16 / (k_ms * 1e-3) / 1e9
+    if args.pmc_json and os.path.exists(args.pmc_json):
+        try:
+            pmc = json.load(open(args.pmc_json))
+            key = f"{args.scene}:{W}x{H}:{params.spp}:{world}:{roof.get('trace_path', 'ubershader')}"
+            if key in pmc:
+                roof["traffic"] = pmc[key]
+        except Exception as e:  # report, don't fail the bench
+            print(f"[bench] pmc json unreadable: {e}", file=sys.stderr)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline and info.mode == wl.MODE_PATHTRACE:
+        cpu = cpu_baseline(r, params, args.cpu_seconds)
+    cfg = {"workload": f"{info.name}: {W}x{H}, {params.spp} spp, {params.max_depth} bounces, "
+                       f"{info.spheres} spheres + {info.halfspaces} half-spaces, {info.binops} binops",
+           "scene": info.name, "width": W, "height": H, "spp": params.spp,
+           "max_depth": params.max_depth, "tile_rows": T}
+    cfg.update(cfg_extra)
+    cfg["hip_runtime"] = wl.load().wo_hip_runtime_version()
+    return {
+        "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": cfg,
+        "fps": round(steps / elapsed_s, 3),
+        "msamples_per_s": round(samples * steps / elapsed_s / 1e6, 3),
+        "segments_per_frame": segs_all // steps,
+        "roofline": roof,
+        "roofline_hbm_store": {"bound": "hbm", "achieved": round(hbm_gbs, 3), "peak": PEAK_HBM_GBS,
+                               "unit": "GB/s", "frac": round(hbm_gbs / PEAK_HBM_GBS, 6)},
+        "cpu_baseline": cpu,
+    }
+
+
+def single_process(args):
+    """N GPUs from one process through the C API: wo_renderer_set_devices(N) puts rank i
+    on device i (its own stream and buffers; ranks stack when N exceeds the visible
+    GPUs, with --stack-ranks), and a step is one wo_renderer_render_frame_device: every
+    rank renders its row-cyclic tiles, ranks 1..N-1 copy their share into rank 0's
+    gather buffer (peer DMA over xGMI), rank 0 assembles the frame in its HBM.
+    Consecutive frames alternate two gather buffers, so frame k+1 renders while frame
+    k is gathered.  The roofline's kernel time is the whole step here (the ranks'
+    launches run on the library's streams)."""
+    import numpy as np
+    import torch
+
+    from csgrenderer_amd import scenes
+    from csgrenderer_amd import wololo as wl
+
+    n = args.gpus
+    ndev = visible_devices()
+    if ndev < n and not args.stack_ranks:
+        fail(f"--single-process --gpus {n} needs {n} GPUs, {ndev} visible (--stack-ranks to rehearse on fewer)")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    r = wl.Renderer("bench-sp", max_nodes=4096)
+    info = scenes.sphere256() if args.scene == "sphere256" else scenes.build(args.scene, r)
+    over = {"max_depth": args.depth}
+    for k in ("width", "height", "spp"):
+        if getattr(args, k):
+            over[k] = getattr(args, k)
+    params = info.params(**over)
+    r.set_tracer("interpreter" if args.jit == 0 else args.tracer)
+    if r.set_devices(n) != n or r.device_count() != n:
+        fail(f"wo_renderer_set_devices({n}) failed: {wl.last_error()}")
+    W, H = params.width, params.height
+    frames = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) for _ in range(2)]
+    cs = torch.cuda.current_stream(dev)
+    fno = [0]
+
+    def step():
+        r.render_frame_device(params, frames[fno[0] & 1].data_ptr(), cs.cuda_stream)
+        fno[0] += 1
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    r.take_segments()  # the warm-up frames' count
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    elapsed_s = t1 - t0
+    segs = r.take_segments()
+    peers = sorted({r.peer_mode(i) for i in range(1, n)}) if n > 1 else []
+    last = frames[(fno[0] - 1) & 1].cpu().numpy()
+    r.set_devices(1)  # the counting frame and the verification render run on one rank
+    work = None
+    if info.mode == wl.MODE_PATHTRACE and not args.no_count_work:
+        work = r.count_work(params, args.tile_rows, 0, 1)
+    verified = None
+    if args.verify:
+        full = r.render(params)
+        verified = bool(np.array_equal(last, full))
+        if not verified:
+            bad = int((last != full).any(axis=-1).sum())
+            print(f"[bench] VERIFY FAILED: {bad} pixels of the assembled frame differ from a one-rank render",
+                  file=sys.stderr)
+    k_ms = elapsed_s / args.steps * 1e3
+    args_rows = args.tile_rows
+    args.tile_rows = 4  # the library's frames use 4-row tiles
+    if n > 1:
+        args.no_cpu_baseline = True  # the CPU baseline is an N = 1 figure
+        args.pmc_json = None  # the committed PMC traffic is per N = 1 launch
+    line = report_line(args, r, info, params, 1, elapsed_s, segs, segs, k_ms, work,
+                       {"parallelism": f"row-cyclic tiles x{n}, one process, C API (wo_renderer_set_devices)"
+                                       + (f", share gather by {'/'.join(peers)}" if peers else "")
+                                       + (f"; {n} ranks stacked on {ndev} GPU(s) (rehearsal)" if ndev < n else ""),
+                        "ranks": n, "devices": min(n, ndev), "launcher": "single-process",
+                        "frames_in_flight": 2})
+    args.tile_rows = args_rows
+    line["n_gpus"] = n
+    line["roofline"]["kernel_ms_basis"] = "whole step (all ranks' launches, gather and assembly)"
+    if verified is not None:
+        line["verified_vs_full_render"] = verified
+    print(json.dumps(line), flush=True)
+    r.close()
+    if verified is False:
         sys.exit(3)
 
 
@@ -336,6 +503,8 @@ def cpu_baseline(r, params, budget_s: float):
         row = (row + n) % params.height
     dt = time.perf_counter() - t0
     return {"value": round(segs / dt / 1e6, 4), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
+            "host_cpus": pyoracle.host_cpus(),
+            "threads_from": "OMP_NUM_THREADS" if os.environ.get("OMP_NUM_THREADS") else "affinity mask",
             "sample": f"{rows} of {params.height} rows (from row {start}, wrapping) of the "
                       f"same {params.width}x{params.height} frame, {params.spp} spp, {params.max_depth} bounces; "
                       f"{segs} segments in {dt:.1f} s"}

@@ -11,7 +11,8 @@
  * second process or rank loads the object instead of compiling it.
  *
  * Location: $WOLOLO_JIT_CACHE (a directory; "0" or "" disables the cache), else
- * $XDG_CACHE_HOME/wololo/jit, else $HOME/.cache/wololo/jit.
+ * $XDG_CACHE_HOME/wololo/jit, else $HOME/.cache/wololo/jit; created 0700, and
+ * not used unless it is owned by this user and writable by nobody else.
  * File: <key>.co = "WOJITCO1" | u64 size | SHA-256(code) | code.  Written to a
  * private temporary name and renamed into place, so concurrent writers (ranks
  * of one node) never expose a partial file; a reader checks the size and the
@@ -132,7 +133,7 @@ static int mkdir_p(const char* path) {
         if (buf[i] == '/' || buf[i] == '\0') {
             char c = buf[i];
             buf[i] = '\0';
-            if (mkdir(buf, 0755) != 0 && errno != EEXIST) return -1;
+            if (mkdir(buf, 0700) != 0 && errno != EEXIST) return -1;
             buf[i] = c;
         }
     }
@@ -156,7 +157,19 @@ int wo_jit_cache_dir(char* out, size_t len) {
             return -1;
     }
     if (n <= 0 || (size_t)n >= len) return -1;
-    return mkdir_p(out);
+    if (mkdir_p(out)) return -1;
+    /* Every object in the directory is loaded and run as GPU code: refuse one
+     * that another user owns or that others can write to (an existing private
+     * cache created with 0755 is fine; new directories are created 0700). */
+    struct stat st;
+    if (stat(out, &st) != 0 || !S_ISDIR(st.st_mode) || st.st_uid != geteuid() || (st.st_mode & 022)) {
+        static int warned;
+        if (!__atomic_exchange_n(&warned, 1, __ATOMIC_RELAXED))
+            fprintf(stderr, WO_LOG_PREFIX " code-object cache %s is not a private directory of this user; "
+                            "cache off\n", out);
+        return -1;
+    }
+    return 0;
 }
 
 static const char kMagic[8] = {'W', 'O', 'J', 'I', 'T', 'C', 'O', '1'};

@@ -17,6 +17,7 @@
  * float bit patterns, which are monotone for v >= 0.
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -33,26 +34,28 @@ static float f_of_bits(uint32_t u) {
     return f;
 }
 
-void wo_srgb8_thresholds(float out[255]) {
-    static float table[255];
-    static int ready = 0;
-    if (!ready) {
-        for (int j = 0; j < 255; ++j) {
-            const double target = (j + 0.5) / 255.0;
-            /* smallest bits b in (0, bits(1.0)] with srgb(f(b)) >= target */
-            uint32_t lo = 0u, hi = 0x3f800000u; /* srgb(0) < target <= srgb(1) */
-            while (hi - lo > 1u) {
-                uint32_t mid = lo + (hi - lo) / 2u;
-                if (srgb_encode_d((double)f_of_bits(mid)) >= target)
-                    hi = mid;
-                else
-                    lo = mid;
-            }
-            table[j] = f_of_bits(hi);
+static float g_srgb_table[255];
+static pthread_once_t g_srgb_once = PTHREAD_ONCE_INIT;
+
+static void build_srgb_table(void) {
+    for (int j = 0; j < 255; ++j) {
+        const double target = (j + 0.5) / 255.0;
+        /* smallest bits b in (0, bits(1.0)] with srgb(f(b)) >= target */
+        uint32_t lo = 0u, hi = 0x3f800000u; /* srgb(0) < target <= srgb(1) */
+        while (hi - lo > 1u) {
+            uint32_t mid = lo + (hi - lo) / 2u;
+            if (srgb_encode_d((double)f_of_bits(mid)) >= target)
+                hi = mid;
+            else
+                lo = mid;
         }
-        ready = 1; /* idempotent: concurrent first calls write the same values */
+        g_srgb_table[j] = f_of_bits(hi);
     }
-    memcpy(out, table, sizeof table);
+}
+
+void wo_srgb8_thresholds(float out[255]) {
+    (void)pthread_once(&g_srgb_once, build_srgb_table); /* built once, whatever thread asks first */
+    memcpy(out, g_srgb_table, sizeof g_srgb_table);
 }
 
 /* Host form of the device encode (same table, same rule): used for the PPM

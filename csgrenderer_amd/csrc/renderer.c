@@ -137,20 +137,61 @@ Wo_Renderer* wo_renderer_new(Wo_App* app, char const* name, size_t max_node_coun
     r->device = dev;
     r->devs[0] = r->dev;
     r->ndevs = 1;
-    /* Ranks per frame: WOLOLO_DEVICES=N|all, else every visible GPU for a
-     * renderer of the app (the demo's, main.c:38) and one for a library caller
-     * (one process per GPU, e.g. bench.py under torchrun). */
-    int want = 1;
+    /* Ranks per frame: WOLOLO_DEVICES=N|all (always N), else every visible GPU
+     * for a renderer of the app (the demo's, main.c:38) with the count chosen
+     * per frame by workload (frame_ranks), and one for a library caller (one
+     * process per GPU, e.g. bench.py under torchrun). */
+    int want = 1, automatic = 0;
     const char* dv = getenv("WOLOLO_DEVICES");
-    if (dv && *dv)
+    if (dv && strncmp(dv, "auto", 4) == 0) {
+        /* the app's rule for any renderer; "auto:N" = N ranks (stacked when N
+         * exceeds the GPUs: how the rule is tested on one GPU) */
+        want = dv[4] == ':' ? atoi(dv + 5) : ndev;
+        automatic = 1;
+    } else if (dv && *dv) {
         want = strcmp(dv, "all") == 0 ? ndev : atoi(dv);
-    else if (app)
+    } else if (app) {
         want = ndev;
+        automatic = 1;
+    }
     if (want > WO_MAX_DEVICES) want = WO_MAX_DEVICES;
-    if (want > 1 && wo_renderer_set_devices(r, want) < 0)
-        fprintf(stderr, WO_LOG_PREFIX " multi-GPU setup failed (%s); rendering on device %d only.\n",
-                wo_renderer_last_error(), dev);
+    if (want > 1) {
+        if (wo_renderer_set_devices(r, want) < 0)
+            fprintf(stderr, WO_LOG_PREFIX " multi-GPU setup failed (%s); rendering on device %d only.\n",
+                    wo_renderer_last_error(), dev);
+        else
+            r->ranks_auto = automatic;
+    }
     return r;
+}
+
+/* Ranks a frame is split over.  Explicit (set_devices, WOLOLO_DEVICES): all of
+ * them.  The app's default: the reference shader, the debug view and normals
+ * frames are a few microseconds of kernel (C1 1080p: 0.019 ms), which n-1 share
+ * copies, event waits and an assembly would only slow down, so they stay on
+ * rank 0; a path-traced frame takes one rank per WOLOLO_RANK_MIN_SAMPLES
+ * samples (default 4 Mi: about 0.1 ms of csg32 kernel per rank). */
+static uint32_t frame_ranks(Wo_Renderer const* r, Wo_RenderParams const* p) {
+    if (r->ndevs <= 1u || !r->ranks_auto) return r->ndevs ? r->ndevs : 1u;
+    if (p->mode != WO_SHADING_PATHTRACE) return 1u;
+    uint64_t per = 1ull << 22;
+    const char* e = getenv("WOLOLO_RANK_MIN_SAMPLES");
+    if (e && *e) per = strtoull(e, NULL, 10);
+    if (per == 0) return r->ndevs;
+    const uint64_t samples = (uint64_t)p->width * p->height * p->spp;
+    uint64_t n = samples / per;
+    if (n < 1) n = 1;
+    return n < r->ndevs ? (uint32_t)n : r->ndevs;
+}
+
+int wo_renderer_frame_ranks(Wo_Renderer* r, Wo_RenderParams const* params) {
+    if (!r || !r->dev || !params) return 0;
+    return (int)frame_ranks(r, params);
+}
+
+int wo_renderer_peer_mode(Wo_Renderer* r, int rank) {
+    if (!r || rank < 1 || (uint32_t)rank >= r->ndevs) return -1;
+    return wo_dev_peer_mode(r->devs[rank]);
 }
 
 /* Row-cyclic frames over n ranks: rank i on HIP device (device + i) mod
@@ -168,6 +209,10 @@ int wo_renderer_set_devices(Wo_Renderer* r, int n) {
     if (wo_renderer_finish(r)) return -1;
     const int ndev = wo_dev_count();
     const int cur = wo_dev_current();
+    r->ranks_auto = 0; /* an explicit count: every frame uses all n ranks */
+    /* fault injection for the tests: rank k's set-up fails (WOLOLO_FAULT_RANK=k) */
+    const char* fk = getenv("WOLOLO_FAULT_RANK");
+    const int fault_rank = fk && *fk ? atoi(fk) : -1;
     for (uint32_t i = 1; i < r->ndevs; ++i) {
         wo_dev_destroy(r->devs[i]);
         r->devs[i] = NULL;
@@ -179,6 +224,11 @@ int wo_renderer_set_devices(Wo_Renderer* r, int n) {
     char err[256] = {0};
     for (int i = 1; i < n; ++i) {
         const int d = ndev > 0 ? (r->device + i) % ndev : r->device;
+        if (i == fault_rank) {
+            wo_set_error("rank %d on device %d: injected fault (WOLOLO_FAULT_RANK)", i, d);
+            rc = -1;
+            break;
+        }
         if (wo_dev_create(d, &r->devs[i], err, sizeof err) != 0) {
             r->devs[i] = NULL;
             wo_set_error("rank %d on device %d: %s", i, d, err);
@@ -443,6 +493,7 @@ static int sync_device(Wo_Renderer* r) {
             if (wo_dev_upload_scene(r->devs[i], r->prog, r->n_recs, r->n_prims, r->mats, r->n_mats, err,
                                     sizeof err)) {
                 wo_set_error("scene upload failed (rank %u): %s", i, err);
+                if (cur >= 0) (void)wo_dev_select(cur); /* the caller's device, on every exit */
                 return -1;
             }
         }
@@ -523,7 +574,7 @@ char const* wo_renderer_trace_path(Wo_Renderer* r) {
 static int render_sync(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba, int accumulate, int reset);
 
 int wo_renderer_render_f32(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba) {
-    if (r && r->ndevs > 1) return render_sync(r, params, out_rgba, 0, 0) < 0 ? -1 : 0;
+    if (r && r->dev && frame_ranks(r, params) > 1u) return render_sync(r, params, out_rgba, 0, 0) < 0 ? -1 : 0;
     if (sync_device(r)) return -1;
     WoFrame fr;
     if (wo_renderer_frame_desc(r, params, 16, 0, 1, &fr)) return -1;
@@ -614,9 +665,10 @@ int wo_renderer_finish(Wo_Renderer* r) {
 
 /* Accumulation bookkeeping shared by draw_frame and render_accumulate: whether
  * this frame continues the accumulation, its sample offset and the total. */
-static int acc_continues(Wo_Renderer* r, Wo_RenderParams const* p) {
+static int acc_continues(Wo_Renderer* r, Wo_RenderParams const* p, uint32_t nranks) {
     Wo_RenderParams a = r->acc_params;
-    return r->acc_valid && r->acc_view == r->view_version && a.width == p->width && a.height == p->height &&
+    return r->acc_valid && r->acc_view == r->view_version && r->acc_ranks == nranks && a.width == p->width &&
+           a.height == p->height &&
            a.spp == p->spp && a.max_depth == p->max_depth && a.seed == p->seed && a.mode == p->mode &&
            a.sample_offset == p->sample_offset;
 }
@@ -626,16 +678,18 @@ static int submit_frame(Wo_Renderer* r, Wo_RenderParams p, int slot, int accumul
     long long* d_acc[WO_MAX_DEVICES] = {NULL};
     int acc = 0;
     uint32_t total = 0;
+    const uint32_t nr = frame_ranks(r, &p);
     if (accumulate && p.mode == WO_SHADING_PATHTRACE) {
-        int cont = !reset && acc_continues(r, &p);
+        int cont = !reset && acc_continues(r, &p, nr);
         if (!cont) {
             r->acc_params = p;
             r->acc_view = r->view_version;
+            r->acc_ranks = nr;
             r->acc_spp = 0;
             r->acc_valid = 1;
         }
-        for (uint32_t i = 0; i < r->ndevs; ++i) {
-            if (wo_dev_accum_prepare(r->devs[i], p.width, p.height, 4, r->ndevs, !cont, &d_acc[i], err, sizeof err)) {
+        for (uint32_t i = 0; i < nr; ++i) {
+            if (wo_dev_accum_prepare(r->devs[i], p.width, p.height, 4, nr, !cont, &d_acc[i], err, sizeof err)) {
                 wo_set_error("accumulation buffer (rank %u): %s", i, err);
                 return -1;
             }
@@ -651,17 +705,19 @@ static int submit_frame(Wo_Renderer* r, Wo_RenderParams p, int slot, int accumul
         r->acc_spp = total;
     }
     WoFrame fr;
-    if (wo_renderer_frame_desc(r, &p, 4, 0, r->ndevs, &fr)) return -1;
+    if (wo_renderer_frame_desc(r, &p, 4, 0, nr, &fr)) return -1;
     const int cur = r->ndevs > 1 ? wo_dev_current() : -1;
-    int rc = wo_dev_frame_submit_ranks(r->devs, r->ndevs, &fr, slot, acc ? d_acc : NULL, total, err, sizeof err);
+    int rc = wo_dev_frame_submit_ranks(r->devs, nr, &fr, slot, acc ? d_acc : NULL, total, err, sizeof err);
     if (cur >= 0) (void)wo_dev_select(cur);
     if (rc) {
         wo_set_error("frame submit failed: %s", err);
         return -1;
     }
-    r->pending[slot] = 1;
-    r->pend_w[slot] = p.width;
-    r->pend_h[slot] = p.height;
+    if (slot <= WO_SLOT_PIPE1) {
+        r->pending[slot] = 1;
+        r->pend_w[slot] = p.width;
+        r->pend_h[slot] = p.height;
+    }
     return 0;
 }
 
@@ -721,18 +777,59 @@ int wo_renderer_render_accumulate(Wo_Renderer* r, Wo_RenderParams const* params,
     return render_sync(r, params, out_rgba, 1, reset);
 }
 
-/* One frame through the pipeline's slot 0, waited for (every rank). */
+/* One frame through the scratch slot (every rank), waited for.  Not presented:
+ * wo_renderer_last_frame keeps pointing at the last presented frame, whose
+ * pipeline slot this does not touch. */
 static int render_sync(Wo_Renderer* r, Wo_RenderParams const* params, float* out_rgba, int accumulate, int reset) {
-    if (wo_renderer_finish(r)) return -1; /* the pipeline's frames first */
+    if (wo_renderer_finish(r)) return -1; /* the pipeline's frames first (in order) */
     if (sync_device(r)) return -1;
-    if (submit_frame(r, *params, 0, accumulate, reset)) return -1;
-    r->pending[0] = 0;
+    if (submit_frame(r, *params, WO_SLOT_SYNC, accumulate, reset)) return -1;
     char err[256] = {0};
     float const* px = NULL;
-    if (wo_dev_frame_wait(r->dev, 0, &px, NULL, err, sizeof err)) {
+    if (wo_dev_frame_wait(r->dev, WO_SLOT_SYNC, &px, NULL, err, sizeof err)) {
         wo_set_error("frame wait failed: %s", err);
         return -1;
     }
     if (out_rgba) memcpy(out_rgba, px, (size_t)params->width * params->height * 4u * sizeof(float));
     return accumulate ? (int)r->acc_spp : 0;
+}
+
+/* ---------------------------------------------------------------- device frames */
+
+int wo_renderer_render_frame_device(Wo_Renderer* r, Wo_RenderParams const* params, void* d_frame, void* stream) {
+    if (!r || !params) return -1;
+    if (sync_device(r)) return -1;
+    const uint32_t nr = frame_ranks(r, params);
+    WoFrame fr;
+    if (wo_renderer_frame_desc(r, params, 4, 0, nr, &fr)) return -1;
+    const int slot = (r->dframe_seq & 1u) ? WO_SLOT_DEV1 : WO_SLOT_DEV0;
+    const int cur = r->ndevs > 1 ? wo_dev_current() : -1;
+    char err[256] = {0};
+    int rc = wo_dev_frame_ranks_device(r->devs, nr, &fr, slot, d_frame, stream, err, sizeof err);
+    if (cur >= 0) (void)wo_dev_select(cur);
+    if (rc) {
+        wo_set_error("device frame failed: %s", err);
+        return -1;
+    }
+    r->dframe_seq++;
+    return 0;
+}
+
+int wo_renderer_take_segments(Wo_Renderer* r, unsigned long long* total) {
+    if (!r || !r->dev || !total) return -1;
+    *total = 0;
+    const int cur = wo_dev_current();
+    char err[256] = {0};
+    int rc = 0;
+    for (uint32_t i = 0; i < r->ndevs; ++i) {
+        unsigned long long t = 0;
+        if (wo_dev_take_segments(r->devs[i], &t, err, sizeof err)) {
+            wo_set_error("rank %u: %s", i, err);
+            rc = -1;
+            break;
+        }
+        *total += t;
+    }
+    if (cur >= 0) (void)wo_dev_select(cur);
+    return rc;
 }

@@ -984,29 +984,35 @@ struct WoDev {
     uint32_t lb_depth;     // internal levels of the lane BVH (<= kLaneDepthMax)
     unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
     unsigned long long* d_work;      // WO_WORK_KINDS totals of a counting launch
-    // progressive accumulation (3 int64 per pixel) and the draw_frame pipeline:
-    // two frame slots, each a device frame, a pinned host copy and an event
+    // progressive accumulation (3 int64 per pixel) and the frame slots (wo_dev.h
+    // WO_SLOT_*): the draw_frame pipeline's two, the synchronous render's scratch
+    // slot and the two device-frame slots; a present slot holds a device frame, a
+    // pinned host copy and an event
     long long* d_accum;
     size_t accum_cap;
-    float4* d_slot[2];
-    size_t dslot_cap[2];
-    float* h_slot[2];
-    size_t hslot_cap[2];
-    uint32_t* d_bgra[2];  // the slot's frame encoded for present (B8G8R8A8 sRGB)
-    size_t dbgra_cap[2];
-    uint32_t* h_bgra[2];
-    size_t hbgra_cap[2];
-    hipEvent_t slot_ev[2];
+    float4* d_slot[WO_SLOTS];
+    size_t dslot_cap[WO_SLOTS];
+    float* h_slot[WO_SLOTS];
+    size_t hslot_cap[WO_SLOTS];
+    uint32_t* d_bgra[WO_SLOTS];  // the slot's frame encoded for present (B8G8R8A8 sRGB)
+    size_t dbgra_cap[WO_SLOTS];
+    uint32_t* h_bgra[WO_SLOTS];
+    size_t hbgra_cap[WO_SLOTS];
+    hipEvent_t slot_ev[WO_SLOTS];
     // several devices per renderer (wo_dev_frame_submit_ranks): on the root,
     // the rank-major buffer the ranks' shares are copied into and the event that
-    // opens a slot to the ranks; on every other rank, its share of the frame and
-    // the event that marks the share copied
-    float4* d_gather[2];
-    size_t dgather_cap[2];
-    hipEvent_t gate_ev[2];
-    float4* d_part[2];
-    size_t dpart_cap[2];
-    hipEvent_t part_ev[2];
+    // opens a slot to the ranks; on every rank, its share of the frame and the
+    // event that marks the share delivered (copied, or staged in host memory)
+    float4* d_gather[WO_SLOTS];
+    size_t dgather_cap[WO_SLOTS];
+    hipEvent_t gate_ev[WO_SLOTS];
+    float4* d_part[WO_SLOTS];
+    size_t dpart_cap[WO_SLOTS];
+    float4* h_part[WO_SLOTS];  // WO_PEER_STAGED: the share's pinned host copy
+    size_t hpart_cap[WO_SLOTS];
+    hipEvent_t part_ev[WO_SLOTS];
+    int peer_mode;  // how this rank's share reaches the root (WO_PEER_*; wo_dev_enable_peer)
+    unsigned long long* d_segacc;  // segments of this rank's device frames (wo_dev_take_segments)
     bool union_only;
     bool lanes_on;
     // scene-specialised kernel (hiprtc)
@@ -1022,6 +1028,11 @@ struct WoDev {
 
 static void set_err(char* err, size_t len, const char* what, hipError_t e) {
     if (err && len) snprintf(err, len, "%s: %s", what, hipGetErrorString(e));
+}
+
+extern "C" int wo_hip_runtime_version(void) {
+    int v = 0;
+    return hipRuntimeGetVersion(&v) == hipSuccess ? v : -1;
 }
 
 extern "C" int wo_dev_count(void) {
@@ -1073,7 +1084,8 @@ extern "C" int wo_dev_create(int device, WoDev** out, char* err, size_t errlen) 
 extern "C" void wo_dev_destroy(WoDev* dev) {
     if (!dev) return;
     (void)hipSetDevice(dev->device);
-    (void)hipStreamSynchronize(dev->stream);
+    // device frames assemble on the caller's stream from this rank's buffers
+    (void)hipDeviceSynchronize();
     if (dev->d_prog) (void)hipFree(dev->d_prog);
     if (dev->d_mats) (void)hipFree(dev->d_mats);
     if (dev->d_frame) (void)hipFree(dev->d_frame);
@@ -1083,7 +1095,9 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
     if (dev->d_segslots) (void)hipFree(dev->d_segslots);
     if (dev->d_work) (void)hipFree(dev->d_work);
     if (dev->d_accum) (void)hipFree(dev->d_accum);
-    for (int i = 0; i < 2; ++i) {
+    if (dev->d_segacc) (void)hipFree(dev->d_segacc);
+    for (int i = 0; i < WO_SLOTS; ++i) {
+        if (dev->h_part[i]) (void)hipHostFree(dev->h_part[i]);
         if (dev->d_slot[i]) (void)hipFree(dev->d_slot[i]);
         if (dev->h_slot[i]) (void)hipHostFree(dev->h_slot[i]);
         if (dev->slot_ev[i]) (void)hipEventDestroy(dev->slot_ev[i]);
@@ -1532,11 +1546,30 @@ extern "C" int wo_dev_upload_scene(WoDev* dev, WoRec const* prog, uint32_t n_rec
 // ---- scene-specialised kernels (hiprtc) ----
 
 // Process-wide cache of compiled code objects (the same scene compiled once per
-// process), in front of the on-disk cache (jit_cache.c) shared by processes.
+// process, loaded on every rank), in front of the on-disk cache (jit_cache.c)
+// shared by processes.  Bounded: the least recently used entries go beyond
+// kJitCacheEntries (an interactive session that edits the scene would otherwise
+// keep every version's object, megabytes each; the disk cache still has them).
+struct JitEntry {
+    std::vector<char> code;
+    uint64_t used;
+};
+static const size_t kJitCacheEntries = 8;
 static std::mutex g_jit_mu;
-static std::unordered_map<std::string, std::vector<char>>& jit_cache() {
-    static std::unordered_map<std::string, std::vector<char>> m;
+static uint64_t g_jit_tick;
+static std::unordered_map<std::string, JitEntry>& jit_cache() {
+    static std::unordered_map<std::string, JitEntry> m;
     return m;
+}
+static void jit_cache_put(const std::string& key, const std::vector<char>& code) {  // g_jit_mu held
+    auto& m = jit_cache();
+    m[key] = JitEntry{code, ++g_jit_tick};
+    while (m.size() > kJitCacheEntries) {
+        auto old = m.begin();
+        for (auto it = m.begin(); it != m.end(); ++it)
+            if (it->second.used < old->second.used) old = it;
+        m.erase(old);
+    }
 }
 
 // Extra hiprtc options from WOLOLO_JIT_FLAGS (space separated), e.g.
@@ -1601,7 +1634,7 @@ static int jit_compile(const char* src, const std::string& arch, bool count, std
 }
 
 // SHA-256 over everything the code object depends on: a format tag, the hiprtc
-// version, the target, the options (WOLOLO_JIT_FLAGS included), the embedded
+// and HIP runtime versions, the target, the options (WOLOLO_JIT_FLAGS included), the embedded
 // headers and the generated source; each part length-prefixed.
 static std::string jit_key(const char* src, const std::string& arch, bool count = false) {
     WoSha256 s;
@@ -1611,10 +1644,14 @@ static std::string jit_key(const char* src, const std::string& arch, bool count 
         wo_sha256_update(&s, &len, sizeof len);
         wo_sha256_update(&s, p, n);
     };
-    part("wololo-jit-1", 12);
-    int vmaj = 0, vmin = 0;
+    part("wololo-jit-2", 12);
+    // the toolchain: hiprtc's major.minor and the HIP runtime's full version
+    // (patch level included: a ROCm update that changes the compiler or the
+    // device libraries misses instead of loading a stale object)
+    int vmaj = 0, vmin = 0, vrt = 0;
     (void)hiprtcVersion(&vmaj, &vmin);
-    const int ver[2] = {vmaj, vmin};
+    (void)hipRuntimeGetVersion(&vrt);
+    const int ver[3] = {vmaj, vmin, vrt};
     part((const char*)ver, sizeof ver);
     part(arch.data(), arch.size());
     for (const std::string& o : jit_options(arch, count)) part(o.data(), o.size());
@@ -1636,7 +1673,8 @@ static int jit_code(const char* src, const std::string& arch, bool count, std::v
         std::lock_guard<std::mutex> lock(g_jit_mu);
         auto it = jit_cache().find(key);
         if (it != jit_cache().end()) {
-            code = it->second;
+            it->second.used = ++g_jit_tick;
+            code = it->second.code;
             origin = 0;
         }
     }
@@ -1653,7 +1691,7 @@ static int jit_code(const char* src, const std::string& arch, bool count, std::v
             (void)wo_jit_disk_store(key.c_str(), code.data(), code.size());  // best effort
         }
         std::lock_guard<std::mutex> lock(g_jit_mu);
-        jit_cache()[key] = code;
+        jit_cache_put(key, code);
     }
     seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return 0;
@@ -2216,9 +2254,11 @@ static int present_slot(WoDev* dev, int slot, size_t pixels, char* err, size_t e
     return 0;
 }
 
+static bool present_slot_ok(int slot) { return slot >= 0 && slot <= WO_SLOT_SYNC; }
+
 extern "C" int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, long long* d_accum,
                                    uint32_t accum_spp, char* err, size_t errlen) {
-    if (slot < 0 || slot > 1) {
+    if (!present_slot_ok(slot)) {
         snprintf(err, errlen, "bad frame slot %d", slot);
         return -1;
     }
@@ -2236,11 +2276,25 @@ extern "C" int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, l
     return present_slot(dev, slot, (size_t)fr.width * fr.height, err, errlen);
 }
 
+extern "C" int wo_dev_peer_mode(WoDev* dev) { return dev ? dev->peer_mode : -1; }
+
 extern "C" int wo_dev_enable_peer(WoDev* from, WoDev* to, char* err, size_t errlen) {
-    if (from->device == to->device) return 0;
+    const char* pv = getenv("WOLOLO_PEER");
+    if (pv && strcmp(pv, "staged") == 0) {
+        from->peer_mode = WO_PEER_STAGED;
+        return 0;
+    }
+    if (from->device == to->device) {
+        from->peer_mode = WO_PEER_SAME;
+        return 0;
+    }
     int can = 0;
     hipError_t e = hipDeviceCanAccessPeer(&can, from->device, to->device);
-    if (e != hipSuccess || !can) return 0;  // the copies then go through the runtime's staging path
+    if (e != hipSuccess || !can) {
+        (void)hipGetLastError();
+        from->peer_mode = WO_PEER_STAGED;  // no peer path: through pinned host memory
+        return 0;
+    }
     e = hipSetDevice(from->device);
     if (e == hipSuccess) e = hipDeviceEnablePeerAccess(to->device, 0);
     if (e == hipErrorPeerAccessAlreadyEnabled) {
@@ -2251,49 +2305,79 @@ extern "C" int wo_dev_enable_peer(WoDev* from, WoDev* to, char* err, size_t errl
         set_err(err, errlen, "hipDeviceEnablePeerAccess", e);
         return -1;
     }
+    from->peer_mode = WO_PEER_DMA;
     return 0;
 }
 
-// A frame over n ranks: rank i renders its row-cyclic 4-row
-// tiles on its own device and stream; ranks 1..n-1 copy their share into the
-// root's rank-major gather buffer (peer DMA over xGMI when the devices differ)
-// and the root un-interleaves the gathered shares into the slot's frame, then
-// presents as for one device.  Every step is asynchronous; the streams are
-// ordered by events only (gate: the slot's previous use on the root is done;
-// part_ev: a rank's copy is done).
-extern "C" int wo_dev_frame_submit_ranks(WoDev* const* devs, uint32_t n, WoFrame const* frame, int slot,
-                                         long long* const* d_accum, uint32_t accum_spp, char* err, size_t errlen) {
-    if (n <= 1u) return wo_dev_frame_submit(devs[0], frame, slot, d_accum ? d_accum[0] : nullptr, accum_spp, err, errlen);
-    if (slot < 0 || slot > 1) {
-        snprintf(err, errlen, "bad frame slot %d", slot);
-        return -1;
-    }
+// A frame over n ranks into the root's device buffer `dst`,
+// assembled on the root-device stream `s_out`: rank i renders its row-cyclic
+// 4-row tiles on its own device and stream once the slot is free (gate: recorded
+// on s_out after the slot's previous assembly, so frame k+1 in the other slot
+// renders while frame k is still being gathered); ranks 1..n-1 deliver their share into the root's rank-major gather
+// buffer (peer DMA over xGMI, a device copy when stacked on the root's device, or
+// through pinned host memory without a peer path) and record part_ev; s_out waits
+// for every part, then un-interleaves the gathered shares into dst.  The root's
+// own share renders on root->stream, straight into its slice of the gather buffer
+// (an event orders it when s_out is another stream).  Asynchronous throughout.
+static int ranks_render_assemble(WoDev* const* devs, uint32_t n, WoFrame fr, int slot, long long* const* d_accum,
+                                 uint32_t accum_spp, hipStream_t s_out, float4* dst, bool count_segments, char* err,
+                                 size_t errlen) {
     WoDev* root = devs[0];
-    WoFrame fr = *frame;
     fr.tile_rows = 4;
     fr.nranks = n;
     const uint32_t lr = wo_rank_local_rows(fr.height, fr.tile_rows, n);
     const size_t share = (size_t)lr * fr.width;  // float4s per rank
-    const size_t pixels = (size_t)fr.width * fr.height;
     hipError_t e = hipSetDevice(root->device);
     if (e != hipSuccess) {
         set_err(err, errlen, "hipSetDevice", e);
         return -1;
     }
-    if (prep_slot(root, slot, fr.width, fr.height, fr.height, err, errlen)) return -1;
     if (ensure_buffer(&root->d_gather[slot], &root->dgather_cap[slot], share * n * sizeof(float4), err, errlen))
         return -1;
-    if (ensure_event(&root->gate_ev[slot], err, errlen)) return -1;
-    e = hipEventRecord(root->gate_ev[slot], root->stream);
-    if (e != hipSuccess) {
-        set_err(err, errlen, "hipEventRecord(gate)", e);
-        return -1;
+    if (!root->gate_ev[slot]) {  // first use of the slot: nothing to wait for beyond what s_out holds
+        if (ensure_event(&root->gate_ev[slot], err, errlen)) return -1;
+        e = hipEventRecord(root->gate_ev[slot], s_out);
+        if (e != hipSuccess) {
+            set_err(err, errlen, "hipEventRecord(gate)", e);
+            return -1;
+        }
     }
+    auto seg_counter = [&](WoDev* dv) -> unsigned long long* {
+        if (!count_segments) return nullptr;
+        if (!dv->d_segacc) {
+            hipError_t m = hipMalloc((void**)&dv->d_segacc, sizeof(unsigned long long));
+            if (m == hipSuccess) m = hipMemset(dv->d_segacc, 0, sizeof(unsigned long long));
+            if (m != hipSuccess) {
+                dv->d_segacc = nullptr;
+                set_err(err, errlen, "hipMalloc(segment counter)", m);
+            }
+        }
+        return dv->d_segacc;
+    };
     // rank 0 renders straight into its slice of the gather buffer
     fr.rank = 0;
-    if (wo_dev_launch_ex(root, &fr, root->d_gather[slot], root->stream, nullptr, d_accum ? d_accum[0] : nullptr,
+    unsigned long long* seg0 = seg_counter(root);
+    if (count_segments && !seg0) return -1;
+    const bool own_stream = s_out != root->stream;
+    if (own_stream) {
+        if (ensure_event(&root->part_ev[slot], err, errlen)) return -1;
+        e = hipStreamWaitEvent(root->stream, root->gate_ev[slot], 0);
+        if (e != hipSuccess) {
+            set_err(err, errlen, "hipStreamWaitEvent(gate)", e);
+            return -1;
+        }
+    }
+    if (wo_dev_launch_ex(root, &fr, root->d_gather[slot], root->stream, seg0, d_accum ? d_accum[0] : nullptr,
                          accum_spp, err, errlen))
         return -1;
+    if (own_stream) {
+        e = hipEventRecord(root->part_ev[slot], root->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s_out, root->part_ev[slot], 0);
+        if (e != hipSuccess) {
+            set_err(err, errlen, "rank 0 share event", e);
+            return -1;
+        }
+    }
     for (uint32_t i = 1; i < n; ++i) {
         WoDev* dv = devs[i];
         fr.rank = i;
@@ -2302,35 +2386,125 @@ extern "C" int wo_dev_frame_submit_ranks(WoDev* const* devs, uint32_t n, WoFrame
             set_err(err, errlen, "hipSetDevice", e);
             return -1;
         }
+        unsigned long long* seg = seg_counter(dv);
+        if (count_segments && !seg) return -1;
         if (ensure_buffer(&dv->d_part[slot], &dv->dpart_cap[slot], share * sizeof(float4), err, errlen)) return -1;
         if (ensure_event(&dv->part_ev[slot], err, errlen)) return -1;
+        const bool staged = dv->peer_mode == WO_PEER_STAGED;
+        if (staged && ensure_pinned((void**)&dv->h_part[slot], &dv->hpart_cap[slot], share * sizeof(float4), err,
+                                    errlen))
+            return -1;
         e = hipStreamWaitEvent(dv->stream, root->gate_ev[slot], 0);
         if (e != hipSuccess) {
             set_err(err, errlen, "hipStreamWaitEvent(gate)", e);
             return -1;
         }
-        if (wo_dev_launch_ex(dv, &fr, dv->d_part[slot], dv->stream, nullptr, d_accum ? d_accum[i] : nullptr,
-                             accum_spp, err, errlen))
+        if (wo_dev_launch_ex(dv, &fr, dv->d_part[slot], dv->stream, seg, d_accum ? d_accum[i] : nullptr, accum_spp,
+                             err, errlen))
             return -1;
-        e = hipMemcpyPeerAsync(root->d_gather[slot] + share * i, root->device, dv->d_part[slot], dv->device,
-                               share * sizeof(float4), dv->stream);
+        float4* slice = root->d_gather[slot] + share * i;
+        if (staged)  // device -> pinned host on the rank, host -> root below
+            e = hipMemcpyAsync(dv->h_part[slot], dv->d_part[slot], share * sizeof(float4), hipMemcpyDeviceToHost,
+                               dv->stream);
+        else if (dv->device == root->device)
+            e = hipMemcpyAsync(slice, dv->d_part[slot], share * sizeof(float4), hipMemcpyDeviceToDevice, dv->stream);
+        else
+            e = hipMemcpyPeerAsync(slice, root->device, dv->d_part[slot], dv->device, share * sizeof(float4),
+                                   dv->stream);
         if (e == hipSuccess) e = hipEventRecord(dv->part_ev[slot], dv->stream);
         if (e == hipSuccess) e = hipSetDevice(root->device);
-        if (e == hipSuccess) e = hipStreamWaitEvent(root->stream, dv->part_ev[slot], 0);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s_out, dv->part_ev[slot], 0);
+        if (e == hipSuccess && staged)
+            e = hipMemcpyAsync(slice, dv->h_part[slot], share * sizeof(float4), hipMemcpyHostToDevice, s_out);
         if (e != hipSuccess) {
-            set_err(err, errlen, "gather copy", e);
+            set_err(err, errlen, staged ? "gather copy (host-staged)" : "gather copy", e);
             return -1;
         }
     }
-    if (wo_dev_assemble(root->d_gather[slot], root->d_slot[slot], fr.width, fr.height, fr.tile_rows, n,
-                        root->stream, err, errlen))
+    if (wo_dev_assemble(root->d_gather[slot], dst, fr.width, fr.height, fr.tile_rows, n, s_out, err, errlen)) return -1;
+    // the slot's buffers are free once the assembly has read them
+    e = hipEventRecord(root->gate_ev[slot], s_out);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipEventRecord(gate)", e);
         return -1;
-    return present_slot(root, slot, pixels, err, errlen);
+    }
+    return 0;
+}
+
+// The draw_frame pipeline over n ranks: the frame is assembled into the slot's
+// device frame on the root's stream and then presented as for one device.
+extern "C" int wo_dev_frame_submit_ranks(WoDev* const* devs, uint32_t n, WoFrame const* frame, int slot,
+                                         long long* const* d_accum, uint32_t accum_spp, char* err, size_t errlen) {
+    if (n <= 1u) return wo_dev_frame_submit(devs[0], frame, slot, d_accum ? d_accum[0] : nullptr, accum_spp, err, errlen);
+    if (!present_slot_ok(slot)) {
+        snprintf(err, errlen, "bad frame slot %d", slot);
+        return -1;
+    }
+    WoDev* root = devs[0];
+    hipError_t e = hipSetDevice(root->device);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipSetDevice", e);
+        return -1;
+    }
+    if (prep_slot(root, slot, frame->width, frame->height, frame->height, err, errlen)) return -1;
+    if (ranks_render_assemble(devs, n, *frame, slot, d_accum, accum_spp, root->stream, root->d_slot[slot], false, err,
+                              errlen))
+        return -1;
+    return present_slot(root, slot, (size_t)frame->width * frame->height, err, errlen);
+}
+
+extern "C" int wo_dev_frame_ranks_device(WoDev* const* devs, uint32_t n, WoFrame const* frame, int slot, void* d_frame,
+                                         void* stream, char* err, size_t errlen) {
+    if (slot != WO_SLOT_DEV0 && slot != WO_SLOT_DEV1) {
+        snprintf(err, errlen, "bad device-frame slot %d", slot);
+        return -1;
+    }
+    if (!d_frame) {
+        snprintf(err, errlen, "no device frame");
+        return -1;
+    }
+    WoDev* root = devs[0];
+    if (n <= 1u) {  // one rank: straight into the caller's frame (rows >= height are not written)
+        WoFrame fr = whole_frame(frame);
+        hipError_t e = hipSetDevice(root->device);
+        if (e != hipSuccess) {
+            set_err(err, errlen, "hipSetDevice", e);
+            return -1;
+        }
+        if (!root->d_segacc) {
+            e = hipMalloc((void**)&root->d_segacc, sizeof(unsigned long long));
+            if (e == hipSuccess) e = hipMemset(root->d_segacc, 0, sizeof(unsigned long long));
+            if (e != hipSuccess) {
+                root->d_segacc = nullptr;
+                set_err(err, errlen, "hipMalloc(segment counter)", e);
+                return -1;
+            }
+        }
+        const bool path = fr.mode == WO_MODE_PATHTRACE || fr.mode == WO_MODE_NORMALS;
+        return wo_dev_launch(root, &fr, d_frame, stream, path ? root->d_segacc : nullptr, err, errlen);
+    }
+    const bool path = frame->mode == WO_MODE_PATHTRACE || frame->mode == WO_MODE_NORMALS;
+    return ranks_render_assemble(devs, n, *frame, slot, nullptr, 0u, (hipStream_t)stream, (float4*)d_frame, path, err,
+                                 errlen);
+}
+
+extern "C" int wo_dev_take_segments(WoDev* dev, unsigned long long* total, char* err, size_t errlen) {
+    *total = 0;
+    if (!dev->d_segacc) return 0;
+    hipError_t e = hipSetDevice(dev->device);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(total, dev->d_segacc, sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemset(dev->d_segacc, 0, sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        set_err(err, errlen, "segment counter", e);
+        return -1;
+    }
+    return 0;
 }
 
 extern "C" int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, uint32_t const** host_bgra8, char* err,
                                  size_t errlen) {
-    if (slot < 0 || slot > 1 || !dev->slot_ev[slot]) {
+    if (!present_slot_ok(slot) || !dev->slot_ev[slot]) {
         snprintf(err, errlen, "frame slot %d was never submitted", slot);
         return -1;
     }

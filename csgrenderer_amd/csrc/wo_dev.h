@@ -18,6 +18,20 @@ extern "C" {
 
 typedef struct WoDev WoDev;
 
+/* Frame slots of a device: the draw_frame pipeline's two (frame k renders while
+ * k-1 is presented), the synchronous render's scratch slot (never presented, so
+ * wo_renderer_last_frame keeps pointing at the last presented frame), and the
+ * two slots device frames alternate over (wo_renderer_render_frame_device). */
+enum { WO_SLOT_PIPE0 = 0, WO_SLOT_PIPE1 = 1, WO_SLOT_SYNC = 2, WO_SLOT_DEV0 = 3, WO_SLOT_DEV1 = 4, WO_SLOTS = 5 };
+
+/* How a non-root rank's share reaches the root (wo_dev_enable_peer):
+ *   SAME    same HIP device: a device-to-device copy;
+ *   DMA     peer access enabled: hipMemcpyPeerAsync over xGMI;
+ *   STAGED  no peer path (hipDeviceCanAccessPeer = 0, or WOLOLO_PEER=staged):
+ *           the share goes through a pinned host buffer, D2H on the rank's
+ *           stream, H2D on the root's. */
+enum { WO_PEER_SAME = 0, WO_PEER_DMA = 1, WO_PEER_STAGED = 2 };
+
 /* Number of HIP devices (0 on error / no driver). */
 int wo_dev_count(void);
 /* Currently selected HIP device, or -1. */
@@ -65,9 +79,23 @@ int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, long long* d
  * wo_dev_frame_wait(devs[0], slot, ...). */
 int wo_dev_frame_submit_ranks(WoDev* const* devs, uint32_t n, WoFrame const* frame, int slot,
                               long long* const* d_accum, uint32_t accum_spp, char* err, size_t errlen);
-/* Let `from`'s device access `to`'s memory directly (no-op on one device, or
- * when the pair has no peer path). */
+/* A frame over n ranks rendered and assembled into the caller's device frame
+ * d_frame (width x height float4, on devs[0]'s device), ordered on `stream`
+ * (a stream of devs[0]'s device): the ranks render on their own streams once
+ * the slot's previous assembly is done, and the assembly is queued on
+ * `stream`.  `slot` is WO_SLOT_DEV0 or _DEV1 (consecutive frames
+ * alternate, so frame k+1 renders while frame k is gathered).  Each rank adds
+ * its traced segments to its own counter (wo_dev_take_segments). */
+int wo_dev_frame_ranks_device(WoDev* const* devs, uint32_t n, WoFrame const* frame, int slot, void* d_frame,
+                              void* stream, char* err, size_t errlen);
+/* Segments traced by this rank's device frames since the last call (waits for
+ * the device; the counter restarts at 0). */
+int wo_dev_take_segments(WoDev* dev, unsigned long long* total, char* err, size_t errlen);
+/* Set how `from`'s share reaches `to` (WO_PEER_*): peer access is enabled when
+ * the devices differ and the pair has a peer path.  WOLOLO_PEER=staged forces
+ * the host-staged path (also between ranks stacked on one device). */
 int wo_dev_enable_peer(WoDev* from, WoDev* to, char* err, size_t errlen);
+int wo_dev_peer_mode(WoDev* dev);
 /* HIP device of a WoDev. */
 int wo_dev_device(WoDev* dev);
 /* Select a HIP device for the calling thread (restoring the caller's). */

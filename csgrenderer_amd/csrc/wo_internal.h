@@ -69,6 +69,8 @@ struct Wo_Renderer {
     WoDev* dev;         /* rank 0: uploads, presents (== devs[0]) */
     uint32_t ndevs;     /* ranks a frame is split over (wo_renderer_set_devices) */
     WoDev* devs[WO_MAX_DEVICES];
+    int ranks_auto;     /* the app's default: ranks per frame chosen by workload */
+    uint64_t dframe_seq;  /* render_frame_device calls (alternating gather slots) */
 
     int tracer;         /* Wo_Tracer */
     int jit_loaded;     /* the device runs the scene-specialised kernel */
@@ -83,6 +85,7 @@ struct Wo_Renderer {
     uint32_t acc_spp;          /* samples per pixel in the accumulation */
     Wo_RenderParams acc_params;
     uint64_t acc_view;
+    uint32_t acc_ranks;        /* ranks the accumulation is split over (per-rank sums) */
 
     /* draw_frame pipeline: frame k renders while frame k-1 is presented */
     int pending[2];

@@ -233,6 +233,101 @@ def build_csg32(r: Renderer, seed: int = 32, width=1920, height=1080, spp=64, un
                      max_depth=8)
 
 
+class NestedShape:
+    """Host mirror of a csg32_nested subtree, for the non-emptiness check
+    (tests/test_scenes.py): leaves are spheres (centre, radius) or axis boxes
+    (centre, half extents); binops carry their operator."""
+
+    def __init__(self, op, a=None, b=None, centre=None, size=None):
+        self.op, self.a, self.b, self.centre, self.size = op, a, b, centre, size
+
+    def contains(self, pts):
+        """Membership of an (n, 3) float64 array of points."""
+        import numpy as np
+        if self.op == "sphere":
+            return ((pts - np.asarray(self.centre)) ** 2).sum(axis=1) <= self.size ** 2
+        if self.op == "box":
+            return (np.abs(pts - np.asarray(self.centre)) <= np.asarray(self.size)).all(axis=1)
+        a, b = self.a.contains(pts), self.b.contains(pts)
+        return {"u": a | b, "i": a & b, "d": a & ~b}[self.op]
+
+    def nodes(self, depth=0):
+        """(depth, node) of every binop, pre-order."""
+        if self.a is None:
+            return []
+        return [(depth, self)] + self.a.nodes(depth + 1) + self.b.nodes(depth + 1)
+
+
+# csg32_nested: the operator of the j-th binop (left to right) at depth d of the
+# balanced tree; the root subtracts, and every level below has both
+# intersections and differences (and unions)
+_NESTED_OPS = "dui"
+
+
+def build_csg32_nested(r: Renderer, seed: int = 3235, width=1920, height=1080, spp=64, mirror=None) -> SceneInfo:
+    """C3 as SURVEY.md §8(d) wrote it: 32 leaves (20 spheres + 12 half-spaces forming two
+    6-plane boxes) in ONE balanced tree with intersections and differences at every
+    level (31 binops, 63 nodes) -- unlike csg32, whose root is a union of small terms
+    that the specialised kernel's union count is built for.
+
+    Placement makes every operation count: a subtree is built to fill a ball (centre,
+    R); a union puts its operands side by side, an intersection overlaps them by most
+    of their size, a difference bites a smaller operand out of the side of a larger
+    one.  tests/test_scenes.py checks on sampled points that every intersection and
+    every difference of the built tree is non-empty and that every difference removes
+    something.  `mirror` (a list) receives the tree's NestedShape."""
+    rng = Pcg32(seed)
+    n_items = 22  # 20 spheres + 2 boxes (a box is a chain of 6 half-space intersections)
+    box_at = {6, 17}
+    pos_at_depth = {}
+    leaf_no = [0]
+
+    def unit():
+        th, ph = rng.uniform(0, 2 * math.pi), math.acos(rng.uniform(-0.6, 0.6))
+        return (math.sin(ph) * math.cos(th), math.cos(ph), math.sin(ph) * math.sin(th))
+
+    def add(c, k, d):
+        return tuple(ci + k * di for ci, di in zip(c, d))
+
+    def build(n, centre, rad, depth):
+        if n == 1:
+            k = leaf_no[0]
+            leaf_no[0] += 1
+            if k in box_at:
+                half = (0.8 * rad, 0.55 * rad, 0.8 * rad)
+                node, planes = _box_extents(r, centre, half)
+                m = r.metal((0.8, 0.85, 0.9), 0.05) if k == 6 else r.lambertian((0.3, 0.5, 0.7))
+                for pl in planes:
+                    r.set_material(pl, m)
+                return (node, (0.0, 0.0, 0.0)), NestedShape("box", centre=centre, size=half)
+            sph = r.sphere(rad)
+            r.set_material(sph, _random_material(r, rng))
+            return (sph, centre), NestedShape("sphere", centre=centre, size=rad)
+        j = pos_at_depth.get(depth, 0)
+        pos_at_depth[depth] = j + 1
+        op = _NESTED_OPS[(depth + j) % 3]
+        d = unit()
+        nl = n // 2
+        if op == "u":
+            (la, ma), (lb, mb) = build(nl, add(centre, -0.45 * rad, d), 0.7 * rad, depth + 1), \
+                build(n - nl, add(centre, 0.45 * rad, d), 0.7 * rad, depth + 1)
+        elif op == "i":
+            (la, ma), (lb, mb) = build(nl, add(centre, -0.15 * rad, d), 1.0 * rad, depth + 1), \
+                build(n - nl, add(centre, 0.15 * rad, d), 1.0 * rad, depth + 1)
+        else:
+            (la, ma), (lb, mb) = build(nl, centre, 1.0 * rad, depth + 1), \
+                build(n - nl, add(centre, 0.6 * rad, d), 0.75 * rad, depth + 1)
+        node = {"u": r.union, "d": r.difference, "i": r.intersection}[op](arg(*la), arg(*lb))
+        return (node, (0.0, 0.0, 0.0)), NestedShape(op, ma, mb)
+
+    (root, _), shape = build(n_items, (0.0, 1.6, 0.0), 2.6, 0)
+    if mirror is not None:
+        mirror.append(shape)
+    r.set_camera((0.0, 2.4, 6.0), (0.0, 1.4, 0.0), (0, 1, 0), 38.0, 0.0, 6.0)
+    return SceneInfo("csg32_nested", spheres=20, halfspaces=12, binops=31, width=width, height=height, spp=spp,
+                     max_depth=8)
+
+
 def build_csg256(r: Renderer, seed: int = 256, shape: str = "balanced", width=1920, height=1080,
                  spp=64, union_only=False) -> SceneInfo:
     """C5: 128 sphere leaves, 127 binops (255 nodes), leaf 0 an RTIOW-style ground
@@ -273,6 +368,7 @@ def build_csg256(r: Renderer, seed: int = 256, shape: str = "balanced", width=19
 SCENES = {
     "rtiow_cover": build_rtiow_cover,
     "csg32": build_csg32,
+    "csg32_nested": build_csg32_nested,
     # csg32's geometry with the differences made unions (an A/B scene for the
     # union-only lane tracer; not a BASELINE config)
     "csg32_union": lambda r, **k: build_csg32(r, union_only=True, **k),

@@ -115,6 +115,10 @@ SIGNATURES = {
     "wo_assemble_rows_device": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_void_p]),
     "wo_renderer_set_devices": (c_int, [c_void_p, c_int]),
     "wo_renderer_device_count": (c_int, [c_void_p]),
+    "wo_renderer_frame_ranks": (c_int, [c_void_p, POINTER(RenderParams)]),
+    "wo_renderer_peer_mode": (c_int, [c_void_p, c_int]),
+    "wo_renderer_render_frame_device": (c_int, [c_void_p, POINTER(RenderParams), c_void_p, c_void_p]),
+    "wo_renderer_take_segments": (c_int, [c_void_p, POINTER(c_ulonglong)]),
     "wo_renderer_finish": (c_int, [c_void_p]),
     "wo_renderer_last_frame": (POINTER(c_float), [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
     "wo_renderer_last_frame_bgra8": (POINTER(c_uint32), [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
@@ -147,6 +151,7 @@ SIGNATURES = {
     "wo_version": (c_char_p, []),
     "wo_abi_layout": (c_size_t, [c_char_p, c_char_p]),
     "wo_hip_device_count": (c_int, []),
+    "wo_hip_runtime_version": (c_int, []),
     "wo_fastmath_check": (c_int, [c_int, c_uint32, c_uint32, POINTER(c_ulonglong), POINTER(c_uint32)]),
 }
 
@@ -358,6 +363,28 @@ class Renderer:
     def device_count(self) -> int:
         return int(self.lib.wo_renderer_device_count(self.ptr))
 
+    def frame_ranks(self, params: RenderParams) -> int:
+        """Ranks a frame with these parameters is split over (wo_renderer_frame_ranks)."""
+        return int(self.lib.wo_renderer_frame_ranks(self.ptr, ctypes.byref(params)))
+
+    def peer_mode(self, rank: int) -> str | None:
+        """How rank `rank`'s share reaches rank 0: "same", "dma" or "staged" (None for rank 0)."""
+        m = self.lib.wo_renderer_peer_mode(self.ptr, int(rank))
+        return None if m < 0 else PEER_MODES[m]
+
+    def render_frame_device(self, params: RenderParams, d_frame: int, stream: int = 0):
+        """Whole frame over the renderer's ranks into device memory (wo_renderer_render_frame_device)."""
+        if self.lib.wo_renderer_render_frame_device(self.ptr, ctypes.byref(params), c_void_p(d_frame),
+                                                    c_void_p(stream or None)):
+            raise WololoError(last_error())
+
+    def take_segments(self) -> int:
+        """Segments traced by render_frame_device frames since the last call (all ranks)."""
+        t = c_ulonglong(0)
+        if self.lib.wo_renderer_take_segments(self.ptr, ctypes.byref(t)):
+            raise WololoError(last_error())
+        return int(t.value)
+
     def finish(self):
         if self.lib.wo_renderer_finish(self.ptr):
             raise WololoError(last_error())
@@ -446,6 +473,7 @@ def abi_layout(type_name: str, field: str | None = None) -> int:
 
 
 JIT_ORIGINS = ("process", "disk", "compiled")
+PEER_MODES = ("same", "dma", "staged")  # wo_dev.h WO_PEER_*
 
 
 def jit_code_object(src: str, arch: str = "gfx950"):

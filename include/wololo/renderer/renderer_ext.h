@@ -93,16 +93,44 @@ int wo_assemble_rows_device(void const* d_gathered, void* d_frame, uint32_t widt
  * one renderer can split every frame over n ranks: rank i renders the
  * row-cyclic 4-row tiles g with g % n == i on HIP device (d0 + i) mod
  * visible devices (d0 = wo_renderer_device), ranks 1..n-1 copy their share to
- * d0 (peer DMA over xGMI), and d0 assembles and presents the frame.  The image
- * is the same bit for bit for every n.  n above the device count stacks ranks
- * on one device.  draw_frame, render_f32 and render_accumulate use every rank;
- * render_rows_device (the caller splits the frame) uses d0 only.
- * Default: WOLOLO_DEVICES=N|all, else all visible GPUs for a renderer created
- * with an app (the demo) and 1 without.  Returns n, or -1 (last_error; the
+ * d0 (peer DMA over xGMI; through pinned host memory when the pair has no peer
+ * path), and d0 assembles and presents the frame.  The image is the same bit
+ * for bit for every n.  n above the device count stacks ranks on one device.
+ * After set_devices(n), draw_frame, render_f32, render_accumulate and
+ * render_frame_device use all n ranks; render_rows_device (the caller splits
+ * the frame) uses d0 only.
+ * Default: WOLOLO_DEVICES=N|all (n ranks, always), else, for a renderer created
+ * with an app (the demo), every visible GPU with the rank count chosen per frame
+ * by workload: the reference shader, the debug view and normals frames (a few
+ * microseconds of kernel) stay on d0, and a path-traced frame takes one rank
+ * per WOLOLO_RANK_MIN_SAMPLES (default 4 Mi) samples, up to all of them; a
+ * renderer without an app gets one rank.  WOLOLO_DEVICES=auto (every GPU) or
+ * auto:N (N ranks) applies the app's workload rule to any renderer.  Returns n,
+ * or -1 (last_error; the
  * renderer then keeps one rank). */
 int wo_renderer_set_devices(Wo_Renderer* r, int n);
 /* Ranks a frame is split over (0 for a device-less renderer). */
 int wo_renderer_device_count(Wo_Renderer* r);
+/* Ranks a frame with these parameters is split over (the workload rule above
+ * for the app's default, else wo_renderer_device_count). */
+int wo_renderer_frame_ranks(Wo_Renderer* r, Wo_RenderParams const* params);
+/* How rank `rank`'s share reaches d0: 0 same device (device copy), 1 peer DMA,
+ * 2 through pinned host memory (no peer path, or WOLOLO_PEER=staged); -1 for
+ * rank 0 or a bad rank. */
+int wo_renderer_peer_mode(Wo_Renderer* r, int rank);
+/* Render a whole frame over the renderer's ranks into DEVICE memory d_frame
+ * (width*height float4s on d0 = wo_renderer_device; row 0 = top), ordered on
+ * HIP stream `stream` of d0 (NULL = its default stream): d_frame is written on
+ * `stream` after the work queued on it before the call, and is complete when
+ * `stream` reaches the point of the call's return.  The ranks render into the
+ * library's own buffers on their own streams, so they may start earlier.
+ * Asynchronous.  Consecutive calls alternate between two gather buffers, so
+ * frame k+1 renders while frame k is gathered.  No present.  The traced CSG
+ * segments are counted per rank (wo_renderer_take_segments). */
+int wo_renderer_render_frame_device(Wo_Renderer* r, Wo_RenderParams const* params, void* d_frame, void* stream);
+/* Segments traced by render_frame_device frames since the last call, summed
+ * over the ranks (waits for their devices; the counters restart at 0). */
+int wo_renderer_take_segments(Wo_Renderer* r, unsigned long long* total);
 
 /* ---- frame pipeline and progressive rendering ----
  * The reference's draw_frame_with_renderer (renderer.c:2085-2219) ends every
@@ -228,6 +256,11 @@ int wo_fastmath_check(int which, uint32_t lo_bits, uint32_t hi_bits, unsigned lo
 char const* wo_version(void);
 /* Number of visible HIP devices (0 when none / no driver). */
 int wo_hip_device_count(void);
+/* Version of the HIP runtime this process uses (hipRuntimeGetVersion, e.g.
+ * 70226015), or -1.  The scene-specialised kernels are compiled by the hiprtc of
+ * the same installation: whichever libamdhip64.so.7 / libhiprtc.so.7 the process
+ * loaded first (a PyTorch wheel bundles its own). */
+int wo_hip_runtime_version(void);
 
 #ifdef __cplusplus
 }

@@ -47,14 +47,21 @@ def load():
     return _lib
 
 
+def host_cpus() -> int:
+    """CPUs this process may run on (sched_getaffinity)."""
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return max(1, os.cpu_count() or 1)
+
+
 def nthreads_default() -> int:
+    """OMP_NUM_THREADS when set (the GPU box sets it to the job's CPU share), else
+    every CPU of the affinity mask."""
     n = os.environ.get("OMP_NUM_THREADS")
     if n and n.isdigit():
         return max(1, int(n))
-    try:
-        return max(1, min(len(os.sched_getaffinity(0)), 16))
-    except AttributeError:
-        return max(1, min(os.cpu_count() or 1, 16))
+    return host_cpus()
 
 
 def ubershader_pixel(x, y, w, h, t, mode=0):

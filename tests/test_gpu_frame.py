@@ -185,3 +185,195 @@ def test_multi_rank_lanes_and_scene_change():
     _cmp(new4, r.render(p), "new scene over 4 ranks")
     assert not np.array_equal(new4, one)
     r.close()
+
+
+# ---- the multi-device code's branches, reached on one GPU ----
+
+def _csg32(name="mdev", w=96, h=54, spp=3, seed=7):
+    r = wl.Renderer(name, max_nodes=4096)
+    info = scenes.build("csg32", r)
+    return r, info.params(width=w, height=h, spp=spp, seed=seed)
+
+
+def _device_frame(r, p):
+    import torch
+    f = torch.full((p.height, p.width, 4), -1.0, dtype=torch.float32, device="cuda")
+    r.render_frame_device(p, f.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return f.cpu().numpy()
+
+
+def test_host_staged_gather_equals_one_device(monkeypatch):
+    """No peer path (hipDeviceCanAccessPeer = 0; forced here with WOLOLO_PEER=staged, which
+    also applies between ranks stacked on one device): each share goes D2H into pinned
+    host memory on its rank's stream and H2D on the root's.  render_f32, the draw_frame
+    pipeline, progressive accumulation and device frames all equal one rank."""
+    monkeypatch.setenv("WOLOLO_PEER", "staged")
+    r, p = _csg32()
+    one = r.render(p)
+    acc1, _ = r.render_accumulate(p, reset=True)
+    acc2, _ = r.render_accumulate(p)
+    assert r.set_devices(3) == 3
+    assert [r.peer_mode(i) for i in range(3)] == [None, "staged", "staged"]
+    _cmp(r.render(p), one, "render_f32, host-staged gather")
+    r.set_draw_params(p)
+    for _ in range(3):
+        r.draw_frame()
+    r.finish()
+    _cmp(r.last_frame(), one, "draw_frame, host-staged gather")
+    g1, _ = r.render_accumulate(p, reset=True)
+    g2, _ = r.render_accumulate(p)
+    _cmp(g1, acc1, "accumulation 1, host-staged")
+    _cmp(g2, acc2, "accumulation 2, host-staged")
+    _cmp(_device_frame(r, p), one, "device frame, host-staged gather")
+    r.close()
+
+
+def test_stacked_ranks_copy_on_device_and_limits():
+    """Ranks beyond the visible GPUs stack on one device (the share is a device copy);
+    a count outside [1, WO_MAX_DEVICES] is refused and leaves the renderer as it was."""
+    r, p = _csg32()
+    one = r.render(p)
+    assert r.set_devices(3) == 3
+    assert [r.peer_mode(i) for i in range(1, 3)] == ["same", "same"]
+    for bad in (0, 17, -1):
+        with pytest.raises(wl.WololoError):
+            r.set_devices(bad)
+        assert r.device_count() == 3
+    _cmp(r.render(p), one, "3 stacked ranks")
+    r.close()
+
+
+def test_set_devices_failing_partway_keeps_one_rank(monkeypatch):
+    """Rank 2 of 4 fails to set up (fault injection): set_devices reports the failure,
+    the ranks it had made are released, and the renderer keeps rendering on one rank,
+    bit-exact, through every entry point."""
+    r, p = _csg32()
+    one = r.render(p)
+    monkeypatch.setenv("WOLOLO_FAULT_RANK", "2")
+    with pytest.raises(wl.WololoError, match="injected fault"):
+        r.set_devices(4)
+    assert r.device_count() == 1
+    monkeypatch.delenv("WOLOLO_FAULT_RANK")
+    wl.clear_error()
+    _cmp(r.render(p), one, "after a failed set_devices")
+    r.set_draw_params(p)
+    r.draw_frame()
+    r.finish()
+    _cmp(r.last_frame(), one, "draw_frame after a failed set_devices")
+    _cmp(_device_frame(r, p), one, "device frame after a failed set_devices")
+    assert r.set_devices(2) == 2  # and a later request succeeds
+    _cmp(r.render(p), one, "2 ranks after the failure")
+    assert wl.last_error() == ""
+    r.close()
+
+
+def test_set_devices_with_a_frame_in_flight():
+    """draw_frame returns with a frame in flight; set_devices first retires it (it is
+    presented as rendered), then frames continue over the new rank count."""
+    r, p = _csg32()
+    one = r.render(p)
+    r.set_draw_params(p)
+    wl.clear_error()
+    r.draw_frame()  # in flight on one rank
+    assert r.set_devices(4) == 4
+    _cmp(r.last_frame(), one, "frame in flight across set_devices (presented)")
+    r.draw_frame()
+    r.draw_frame()
+    assert r.set_devices(2) == 2  # back down with frames in flight over 4 ranks
+    _cmp(r.last_frame(), one, "frame in flight across 4 -> 2 ranks")
+    r.draw_frame()
+    r.finish()
+    _cmp(r.last_frame(), one, "draw_frame over 2 ranks")
+    assert wl.last_error() == ""
+    r.close()
+
+
+def test_sync_render_keeps_the_presented_frame():
+    """render_f32 / render_accumulate over several ranks run in their own
+    scratch slot, so last_frame() and last_frame_bgra8() keep the last presented frame."""
+    r, p = _csg32()
+    q = wl.render_params(p.width, p.height, spp=1, mode=wl.MODE_NORMALS)
+    for n in (1, 2):
+        r.set_devices(n)
+        r.set_draw_params(p)
+        r.draw_frame()
+        r.draw_frame()
+        r.finish()
+        shown, shown8 = r.last_frame(), r.last_frame_bgra8()
+        other = r.render(q)
+        r.render_accumulate(p, reset=True)
+        assert not np.array_equal(other, shown)
+        assert np.array_equal(r.last_frame(), shown), f"{n} ranks: render_f32 changed the presented frame"
+        assert np.array_equal(r.last_frame_bgra8(), shown8)
+    r.close()
+
+
+def test_device_frames_over_ranks_pipelined():
+    """wo_renderer_render_frame_device over 1, 2 and 5 stacked ranks: consecutive frames
+    alternate two gather buffers (frame k+1 renders while frame k is gathered); every
+    frame equals one rank's render, and the per-rank segment counters add up to the
+    frame's segment count on one rank."""
+    import torch
+    r, p = _csg32(w=203, h=117)
+    one = r.render(p)
+    seg = torch.zeros(1, dtype=torch.int64, device="cuda")
+    full = torch.empty((p.height, p.width, 4), dtype=torch.float32, device="cuda")
+    r.render_rows_device(p, full.data_ptr(), 4, 0, 1, torch.cuda.current_stream().cuda_stream, seg.data_ptr())
+    torch.cuda.synchronize()
+    segs_one = int(seg.item())
+    for n in (1, 2, 5):
+        r.set_devices(n)
+        r.take_segments()
+        fr = [torch.full((p.height, p.width, 4), -1.0, dtype=torch.float32, device="cuda") for _ in range(4)]
+        s = torch.cuda.current_stream().cuda_stream
+        for f in fr:  # four frames queued back to back
+            r.render_frame_device(p, f.data_ptr(), s)
+        torch.cuda.synchronize()
+        for k, f in enumerate(fr):
+            _cmp(f.cpu().numpy(), one, f"device frame {k} over {n} ranks")
+        assert r.take_segments() == 4 * segs_one
+    r.close()
+
+
+def test_auto_rank_rule_keeps_the_reference_shader_on_one_device(monkeypatch):
+    """The app's default (WOLOLO_DEVICES=auto:8 applies it here with 8 ranks stacked on
+    this GPU): the reference shader at the demo's 1280x720 stays on rank 0, a small
+    path-traced frame too, a 1080p64 frame takes all 8; and the demo frame over 8
+    explicit ranks is slower than over the one the rule picks."""
+    import time
+    monkeypatch.setenv("WOLOLO_DEVICES", "auto:8")
+    r = wl.Renderer("Test1Render", max_nodes=8)
+    s1, s2 = r.sphere(1.0), r.sphere(1.0)
+    r.union(wl.arg(s1), wl.arg(s2))
+    demo = wl.render_params(1280, 720, time_sec=0.25)
+    assert r.device_count() == 8
+    assert r.frame_ranks(demo) == 1
+    assert r.frame_ranks(wl.render_params(1280, 720, spp=1, mode=wl.MODE_PATHTRACE)) == 1
+    assert r.frame_ranks(wl.render_params(1920, 1080, spp=64, mode=wl.MODE_PATHTRACE)) == 8
+    ref = r.render(demo)
+
+    def draw_ms(frames=20, trials=3):
+        r.set_draw_params(demo)
+        r.draw_frame()
+        r.finish()
+        best = None
+        for _ in range(trials):
+            t0 = time.perf_counter()
+            for _ in range(frames):
+                r.draw_frame()
+            r.finish()
+            ms = (time.perf_counter() - t0) / frames * 1e3
+            best = ms if best is None else min(best, ms)
+        return best
+
+    auto_ms = draw_ms()
+    _cmp(r.last_frame(), ref, "demo frame, auto rule")
+    monkeypatch.delenv("WOLOLO_DEVICES")
+    r.set_devices(8)  # explicit: every frame over all 8
+    assert r.frame_ranks(demo) == 8
+    eight_ms = draw_ms()
+    _cmp(r.last_frame(), ref, "demo frame over 8 explicit ranks")
+    print(f"demo 1280x720 draw_frame: auto (1 rank) {auto_ms:.3f} ms, 8 stacked ranks {eight_ms:.3f} ms")
+    assert auto_ms < eight_ms
+    r.close()

@@ -173,11 +173,13 @@ def test_persistent_code_object_cache(hostonly, tmp_path, monkeypatch):
     # off switch
     off = _child(tmp_path, src, {"WOLOLO_JIT_CACHE": "0"})
     assert off["origin"] == "compiled"
-    # same process: the process cache
+    # same process: the process cache.  (Its key may differ from the child's: the key
+    # holds the loaded HIP runtime's version, and this process imported torch, whose
+    # bundled HIP runtime / hiprtc / comgr then serve libwololo too -- another compiler.)
     monkeypatch.setenv("WOLOLO_JIT_CACHE", str(tmp_path / "cache"))
     n, origin, _, key = wl.jit_code_object(src, "gfx950")
     n2, origin2, _, key2 = wl.jit_code_object(src, "gfx950")
-    assert origin2 == "process" and key2 == key == first["key"] and n2 == n
+    assert origin2 == "process" and key2 == key and n2 == n
 
 
 _RENDER_CHILD = r"""

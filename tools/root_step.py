@@ -1,0 +1,150 @@
+#!/usr/bin/env python3
+"""Rank 0's whole per-frame step of an N-GPU frame, timed on ONE GPU (VERDICT r2
+item 2), next to every other rank's share.
+
+An N-GPU frame (bench.py's RCCL path, or wo_renderer_set_devices' peer-DMA path) costs
+rank 0 more than its share of the render: it also receives N-1 shares, un-interleaves
+the frame (assemble_kernel) and, for a presented frame, encodes it (srgb8_kernel).  Per
+frame, on rank 0's GPU:
+
+    render stream:   rank 0's share -> its slice of the gather buffer
+    copy stream:     after the render, N-1 device copies of a share's bytes into the
+                     other slices (stands in for the incoming peer DMA; a local copy
+                     reads and writes this HBM, the real transfer only writes it:
+                     conservative)
+    assemble stream: after the copies, assemble_kernel into the frame + the sRGB
+                     encode (with --no-encode: the bench's frame, which is not
+                     presented)
+
+two frames in flight (two gather buffers, two render streams), F frames back to back.
+Every other rank's step is its share alone, timed the same way (back to back over two
+streams).  Projected N-GPU frame time = max(rank 0's step, the slowest other share);
+speed-up = one GPU's frame time (the N = 1 bench's way: back to back, one stream) over
+it.
+
+    python tools/root_step.py --scene csg32 --worlds 2 4 8
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="csg32")
+    ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
+    ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--no-encode", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    from csgrenderer_amd import scenes
+    from csgrenderer_amd import wololo as wl
+
+    torch.cuda.set_device(0)
+    r = wl.Renderer("root-step", max_nodes=4096)
+    info = scenes.build(args.scene, r)
+    over = {k: getattr(args, k) for k in ("width", "height", "spp") if getattr(args, k)}
+    p = info.params(**over)
+    W, H, T, F = p.width, p.height, 4, args.frames
+    main_s = torch.cuda.current_stream()
+
+    def timed(fn):
+        best = None
+        for _ in range(args.reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            a.record(main_s)
+            fn(a)
+            b.record(main_s)
+            b.synchronize()
+            ms = a.elapsed_time(b) / F
+            best = ms if best is None else min(best, ms)
+        return best
+
+    # one GPU, the whole frame back to back on one stream (bench.py N = 1)
+    full = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+    r.render_rows_device(p, full.data_ptr(), T, 0, 1, main_s.cuda_stream)  # warm-up (JIT)
+    torch.cuda.synchronize()
+
+    def one_gpu(start):
+        for _ in range(F):
+            r.render_rows_device(p, full.data_ptr(), T, 0, 1, main_s.cuda_stream)
+
+    t1 = timed(one_gpu)
+    print(f"[root] N=1 {t1:.3f} ms per frame", flush=True)
+    res = {"scene": args.scene, "size": f"{W}x{H}x{p.spp}", "path": r.trace_path(), "one_gpu_ms": round(t1, 4),
+           "encode": not args.no_encode, "worlds": {}}
+    for n in args.worlds:
+        lr = wl.local_rows(H, T, n)
+        share_bytes = lr * W * 16
+        rs = [torch.cuda.Stream(), torch.cuda.Stream()]
+        cps, asm = torch.cuda.Stream(), torch.cuda.Stream()
+        gather = [torch.empty((n, lr, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
+        frames = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
+        bgra = [torch.empty((H, W), dtype=torch.int32, device="cuda") for _ in range(2)]
+        src = torch.zeros((lr, W, 4), dtype=torch.float32, device="cuda")
+
+        def share(rank):
+            def go(start):
+                for st in rs:
+                    st.wait_event(start)
+                for k in range(F):
+                    r.render_rows_device(p, gather[k & 1][0].data_ptr(), T, rank, n, rs[k & 1].cuda_stream)
+                for st in rs:
+                    main_s.wait_stream(st)
+            return go
+
+        def root(start):
+            for st in rs + [cps, asm]:
+                st.wait_event(start)
+            released = [None, None]
+            for k in range(F):
+                b = k & 1
+                if released[b] is not None:
+                    rs[b].wait_event(released[b])
+                r.render_rows_device(p, gather[b][0].data_ptr(), T, 0, n, rs[b].cuda_stream)
+                done = torch.cuda.Event()
+                done.record(rs[b])
+                cps.wait_event(done)
+                with torch.cuda.stream(cps):
+                    for i in range(1, n):
+                        gather[b][i].copy_(src, non_blocking=True)
+                copied = torch.cuda.Event()
+                copied.record(cps)
+                asm.wait_event(copied)
+                wl.assemble_rows_device(gather[b].data_ptr(), frames[b].data_ptr(), W, H, T, n, asm.cuda_stream)
+                if not args.no_encode:
+                    wl.srgb8_encode_device(frames[b].data_ptr(), bgra[b].data_ptr(), W * H, asm.cuda_stream)
+                ev = torch.cuda.Event()
+                ev.record(asm)
+                released[b] = ev
+            for st in rs + [cps, asm]:
+                main_s.wait_stream(st)
+
+        root(torch.cuda.Event())  # first use of the streams and buffers, untimed
+        torch.cuda.synchronize()
+        root_ms = timed(root)
+        others = [timed(share(k)) for k in range(1, n)]
+        worst_other = max(others) if others else 0.0
+        proj = max(root_ms, worst_other)
+        res["worlds"][n] = {"root_step_ms": round(root_ms, 4), "other_share_ms": [round(x, 4) for x in others],
+                            "share_bytes": share_bytes, "projected_frame_ms": round(proj, 4),
+                            "projected_speedup": round(t1 / proj, 3)}
+        print(f"[root] N={n} rank 0 step {root_ms:.3f} ms (share + {n - 1} copies of {share_bytes / 1e6:.1f} MB "
+              f"+ assemble{'' if args.no_encode else ' + encode'}), slowest other share {worst_other:.3f} ms "
+              f"-> {proj:.3f} ms per frame, {t1 / proj:.2f}x", flush=True)
+    print(json.dumps(res))
+    r.close()
+
+
+if __name__ == "__main__":
+    main()
