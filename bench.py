@@ -114,12 +114,6 @@ def self_launch(args) -> int:
 
 def main():
     args = parse()
-    if os.environ.get("WOLOLO_LOAD_FIRST") == "1":
-        # libwololo (and with it the ROCm installation's HIP runtime, hiprtc and comgr)
-        # before torch, whose wheel bundles its own: torch then shares the ones loaded
-        # here, and the specialised kernels compile with this image's ROCm
-        from csgrenderer_amd import wololo as _wl
-        _wl.load()
     world_env = os.environ.get("WORLD_SIZE")
     if args.single_process:
         if world_env not in (None, "1"):
@@ -141,7 +135,7 @@ def main():
              f"rehearses them on fewer)")
     if ndev < world and args.dist_backend == "nccl":
         fail("RCCL cannot put two ranks on one GPU: stacked ranks need --dist-backend gloo")
-    stacked = ndev < world
+    ranks_stacked = ndev < world
     dev_index = local_rank % max(ndev, 1)
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
@@ -280,7 +274,7 @@ def main():
     if rank == 0:
         parallelism = (f"row-cyclic tiles x{world}" + (f" + {'gloo (host-staged)' if gloo else 'RCCL'} gather" if world > 1 else "")
                        + (" overlapped with the next frame's render" if pipelined else "")
-                       + (f"; {world} ranks stacked on {ndev} GPU(s) (rehearsal)" if stacked else ""))
+                       + (f"; {world} ranks stacked on {ndev} GPU(s) (rehearsal)" if ranks_stacked else ""))
         line = report_line(args, r, info, params, world, elapsed_s, segs_all, segs_local, k_ms, work,
                            {"parallelism": parallelism, "ranks": world, "devices": min(world, ndev),
                             "launcher": "torchrun" if world_env else "none",

@@ -1393,15 +1393,6 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         const char* v = getenv("WOLOLO_JIT_LDS_PROG");
         if (v && *v) lds_prog = v[0] != '0';
     }
-    /* the register window for deep trees holds 5 events (csg256 chain 29.5 ms at 4,
-     * 27.6 at 6, 27.5 at 8; with decision lists 19.36 at 4, 18.47 at 5, 18.65 at 6) */
-    if (!g.lds_events) bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW 5\n#endif\n");
-    /* small scenes run 8 waves per SIMD: a 7-entry LDS list keeps 8 workgroups'
-     * LDS within the CU (csg32 5.24 -> 5.19 ms; csg256 balanced keeps 8 entries:
-     * 15.12 vs 15.33 ms at 7) */
-    if (g.lds_events && n_prims <= 64u) bput(&b, "#ifndef WO_LDS_EVENTS\n#define WO_LDS_EVENTS 7\n#endif\n");
-    bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
-         g.lds_events, tree_depth(prog, n_recs), lds_prog);
     /* the incremental union count's term table, per primitive: its term's mask test */
     uint32_t n_uterms = 0, eval_ops = 0;
     UTerm* uterms = NULL;
@@ -1411,6 +1402,20 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         else n_uterms = union_terms(prog, n_recs, n_prims, uterms, n_prims);
         if (n_uterms < (g.union_count >= 2 ? 1u : 8u)) n_uterms = 0;
     }
+    /* A full LDS event list keeps its smallest keys (WO_LDS_KEEP_SMALLEST): csg32_nested
+     * 20.18 -> 10.97 ms (re-collects per segment 0.86 -> 0.18).  A union of small
+     * terms (csg32, csg256 balanced) rarely fills the list, and there the eviction
+     * code costs csg32 3.608 -> 3.701 ms: off for the union count. */
+    if (g.lds_events && n_uterms) bput(&b, "#ifndef WO_LDS_KEEP_SMALLEST\n#define WO_LDS_KEEP_SMALLEST 0\n#endif\n");
+    /* the register window for deep trees holds 5 events (csg256 chain 29.5 ms at 4,
+     * 27.6 at 6, 27.5 at 8; with decision lists 19.36 at 4, 18.47 at 5, 18.65 at 6) */
+    if (!g.lds_events) bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW 5\n#endif\n");
+    /* small scenes run 8 waves per SIMD: a 7-entry LDS list keeps 8 workgroups'
+     * LDS within the CU (csg32 5.24 -> 5.19 ms; csg256 balanced keeps 8 entries:
+     * 15.12 vs 15.33 ms at 7) */
+    if (g.lds_events && n_prims <= 64u) bput(&b, "#ifndef WO_LDS_EVENTS\n#define WO_LDS_EVENTS 7\n#endif\n");
+    bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
+         g.lds_events, tree_depth(prog, n_recs), lds_prog);
     if (n_uterms) {
         bput(&b, "struct __attribute__((aligned(16))) WoUTerm { uint64_t m, q; uint32_t w, neg, pad0, pad1; };\n");
         bput(&b, "// root = union of %u literal-set terms: a term is true iff ((window(w) & m) == q) != neg,\n"

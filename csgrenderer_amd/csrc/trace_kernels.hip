@@ -1030,6 +1030,14 @@ static void set_err(char* err, size_t len, const char* what, hipError_t e) {
     if (err && len) snprintf(err, len, "%s: %s", what, hipGetErrorString(e));
 }
 
+// Zero device memory and wait for it: hipMemset may still be running on the null
+// stream when a kernel on one of the non-blocking streams starts, and a late
+// memset would wipe what that kernel counted.  (One-time set-ups only.)
+static hipError_t zero_now(void* p, size_t bytes) {
+    hipError_t e = hipMemset(p, 0, bytes);
+    return e == hipSuccess ? hipDeviceSynchronize() : e;
+}
+
 extern "C" int wo_hip_runtime_version(void) {
     int v = 0;
     return hipRuntimeGetVersion(&v) == hipSuccess ? v : -1;
@@ -1977,7 +1985,7 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
             if (!dev->d_segslots) {
                 e = hipMalloc((void**)&dev->d_segslots, kSegSlots * kSegStride * sizeof(unsigned long long));
                 if (e == hipSuccess)
-                    e = hipMemset(dev->d_segslots, 0, kSegSlots * kSegStride * sizeof(unsigned long long));
+                    e = zero_now(dev->d_segslots, kSegSlots * kSegStride * sizeof(unsigned long long));
                 if (e != hipSuccess) {
                     dev->d_segslots = nullptr;
                     set_err(err, errlen, "hipMalloc(segment slots)", e);
@@ -2346,7 +2354,7 @@ static int ranks_render_assemble(WoDev* const* devs, uint32_t n, WoFrame fr, int
         if (!count_segments) return nullptr;
         if (!dv->d_segacc) {
             hipError_t m = hipMalloc((void**)&dv->d_segacc, sizeof(unsigned long long));
-            if (m == hipSuccess) m = hipMemset(dv->d_segacc, 0, sizeof(unsigned long long));
+            if (m == hipSuccess) m = zero_now(dv->d_segacc, sizeof(unsigned long long));
             if (m != hipSuccess) {
                 dv->d_segacc = nullptr;
                 set_err(err, errlen, "hipMalloc(segment counter)", m);
@@ -2473,7 +2481,7 @@ extern "C" int wo_dev_frame_ranks_device(WoDev* const* devs, uint32_t n, WoFrame
         }
         if (!root->d_segacc) {
             e = hipMalloc((void**)&root->d_segacc, sizeof(unsigned long long));
-            if (e == hipSuccess) e = hipMemset(root->d_segacc, 0, sizeof(unsigned long long));
+            if (e == hipSuccess) e = zero_now(root->d_segacc, sizeof(unsigned long long));
             if (e != hipSuccess) {
                 root->d_segacc = nullptr;
                 set_err(err, errlen, "hipMalloc(segment counter)", e);
@@ -2494,7 +2502,7 @@ extern "C" int wo_dev_take_segments(WoDev* dev, unsigned long long* total, char*
     hipError_t e = hipSetDevice(dev->device);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(total, dev->d_segacc, sizeof(unsigned long long), hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemset(dev->d_segacc, 0, sizeof(unsigned long long));
+    if (e == hipSuccess) e = zero_now(dev->d_segacc, sizeof(unsigned long long));
     if (e != hipSuccess) {
         set_err(err, errlen, "segment counter", e);
         return -1;

@@ -450,7 +450,7 @@ def test_jit_event_windows(window, monkeypatch):
     monkeypatch.setenv("WOLOLO_JIT_LDS_EVENTS", "0" if window == "registers" else "1")
     if window == "lds2":
         monkeypatch.setenv("WOLOLO_JIT_FLAGS", "-DWO_LDS_EVENTS=2")
-    for name in ["csg32", "csg256_chain"]:
+    for name in ["csg32", "csg32_nested", "csg256_chain"]:
         r, info = _scene(name, "jit")
         p = info.params(width=64, height=36, spp=4, seed=11)
         img = r.render(p)
@@ -470,6 +470,8 @@ def test_jit_event_windows(window, monkeypatch):
     {"WOLOLO_JIT_SPATIAL": "1"},  # spatial groups instead of the union clusters' bounds
     {"WOLOLO_JIT_SPATIAL": "1", "WOLOLO_JIT_SPATIAL_LEAF": "1"},
     {"WOLOLO_JIT_SPATIAL": "0", "WOLOLO_JIT_UNION_COUNT": "0", "WOLOLO_JIT_DL_EVAL": "0"},
+    {"WOLOLO_JIT_FLAGS": "-DWO_LDS_KEEP_SMALLEST=0"},  # a full event list keeps its first keys
+    {"WOLOLO_JIT_FLAGS": "-DWO_LDS_EVENTS=3"},  # ... or its 3 smallest (overflow on most nested rays)
 ])
 def test_jit_culling_knobs(knobs, monkeypatch):
     """The wave-level member skip, the bound-around-a-lone-primitive rule, the
@@ -479,7 +481,7 @@ def test_jit_culling_knobs(knobs, monkeypatch):
     cube, csg256 balanced's 21 sphere intersections)."""
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)
-    for name in ["csg32", "csg256_balanced"]:
+    for name in ["csg32", "csg32_nested", "csg256_balanced"]:
         r, info = _scene(name, "jit")
         p = info.params(width=64, height=36, spp=4, seed=13)
         img = r.render(p)
