@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scene", default="csg32",
-                    choices=["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain", "csg32_union", "csg256_balanced_union",
+                    choices=["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain", "csg512_balanced", "csg32_union", "csg256_balanced_union",
                              "sphere256"])
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)

@@ -59,6 +59,8 @@ static int env_flag(const char* name) {
     return v && *v && strcmp(v, "0") != 0;
 }
 
+static void jit_old_reap(Wo_Renderer* r, int wait);
+
 /* ---------------------------------------------------------------- lifecycle */
 
 Wo_Renderer* wo_renderer_new(Wo_App* app, char const* name, size_t max_node_count) {
@@ -113,6 +115,7 @@ Wo_Renderer* wo_renderer_new(Wo_App* app, char const* name, size_t max_node_coun
         if (t && strcmp(t, "lanes") == 0) r->tracer = WO_TRACER_LANES;
     }
     r->device = -1;
+    r->jit_async = !(getenv("WOLOLO_JIT_ASYNC") && strcmp(getenv("WOLOLO_JIT_ASYNC"), "0") == 0);
 
     char err[256] = {0};
     int ndev = wo_dev_count();
@@ -258,6 +261,9 @@ int wo_renderer_device_count(Wo_Renderer* r) { return r && r->dev ? (int)r->ndev
 void wo_renderer_del(Wo_Renderer* r) {
     if (!r) return;
     (void)wo_renderer_finish(r);
+    if (r->jit_job) (void)wo_jit_job_finish(r->jit_job, NULL, 0);
+    jit_old_reap(r, 1);
+    free(r->jit_want);
     for (uint32_t i = 1; i < r->ndevs; ++i) wo_dev_destroy(r->devs[i]);
     if (r->dev) wo_dev_destroy(r->dev);
     free(r->nodes);
@@ -473,14 +479,76 @@ int wo_renderer_frame_desc(Wo_Renderer* r, Wo_RenderParams const* p, uint32_t ti
     return 0;
 }
 
-static int sync_device(Wo_Renderer* r) {
+/* ---- background compiles of the specialised kernel ----
+ * A scene edit used to stall draw_frame for the hiprtc compile (csg32 ~1 s, csg256
+ * ~4 s on the box).  draw_frame now starts the compile on a host thread when the
+ * code object is in neither cache and renders with the interpreter (the same
+ * image bit for bit) until it has ended; the next frame after that loads it.
+ * Batch renders (render_f32, render_rows_device, ...) wait for it instead. */
+
+static void jit_old_reap(Wo_Renderer* r, int wait) {
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < r->n_jit_old; ++i) {
+        if (wait || wo_jit_job_done(r->jit_old[i]))
+            (void)wo_jit_job_finish(r->jit_old[i], NULL, 0); /* an edited scene's object: cached, unused */
+        else
+            r->jit_old[k++] = r->jit_old[i];
+    }
+    r->n_jit_old = k;
+}
+
+/* Load the current scene's specialised kernel on every rank once its background
+ * compile has ended (`wait`: wait for it). */
+static void jit_job_poll(Wo_Renderer* r, int wait) {
+    jit_old_reap(r, 0);
+    if (!r->jit_job || (!wait && !wo_jit_job_done(r->jit_job))) return;
+    char err[512] = {0};
+    const int rc = wo_jit_job_finish(r->jit_job, err, sizeof err);
+    r->jit_job = NULL;
+    char* src = r->jit_want;
+    r->jit_want = NULL;
+    if (rc) {
+        fprintf(stderr, WO_LOG_PREFIX " scene specialisation failed (%s); using the interpreter kernel\n", err);
+    } else if (src && !r->dev_stale) {
+        const int cur = r->ndevs > 1 ? wo_dev_current() : -1;
+        int ok = 1;
+        for (uint32_t i = 0; i < r->ndevs && ok; ++i) /* the process cache has it now */
+            if (wo_dev_set_jit(r->devs[i], src, err, sizeof err) != 0) {
+                fprintf(stderr, WO_LOG_PREFIX " loading the specialised kernel failed (%s)\n", err);
+                ok = 0;
+            }
+        if (!ok)
+            for (uint32_t i = 0; i < r->ndevs; ++i) (void)wo_dev_set_jit(r->devs[i], NULL, err, sizeof err);
+        r->jit_loaded = ok;
+        if (cur >= 0) (void)wo_dev_select(cur);
+    }
+    free(src);
+}
+
+/* The compile in flight belongs to an edited scene: let it finish on its own. */
+static void jit_job_orphan(Wo_Renderer* r) {
+    if (!r->jit_job) return;
+    if (r->n_jit_old == sizeof r->jit_old / sizeof r->jit_old[0]) jit_old_reap(r, 1);
+    r->jit_old[r->n_jit_old++] = r->jit_job;
+    r->jit_job = NULL;
+    free(r->jit_want);
+    r->jit_want = NULL;
+}
+
+int wo_renderer_jit_pending(Wo_Renderer* r) { return r && r->jit_job ? 1 : 0; }
+
+/* `may_defer`: the caller renders with the interpreter rather than wait for a
+ * compile (draw_frame). */
+static int sync_device_ex(Wo_Renderer* r, int may_defer) {
     if (!r->dev) {
         wo_set_error("renderer has no HIP device (created with WOLOLO_ALLOW_NO_DEVICE)");
         fprintf(stderr, WO_LOG_PREFIX " render called on a device-less renderer.\n");
         return -1;
     }
     if (wo_renderer_compile(r) < 0) return -1;
+    if (!r->dev_stale) jit_job_poll(r, !may_defer);
     if (r->dev_stale) {
+        jit_job_orphan(r);
         char err[256] = {0};
         /* The pipeline may still hold a frame of the old scene on the device
          * stream (draw_frame returns with one in flight): retire it first, so it
@@ -513,10 +581,15 @@ static int sync_device(Wo_Renderer* r) {
         int want_jit = !want_lanes && r->tracer != WO_TRACER_INTERPRETER && r->n_prims > 0 && r->n_prims <= max_prims;
         for (uint32_t i = 0; i < r->ndevs; ++i) wo_dev_set_lanes(r->devs[i], want_lanes);
         r->lanes_loaded = want_lanes;
+        int deferred = 0;
         if (want_jit) {
             char* src = wo_generate_jit_source(r->prog, r->n_recs, r->n_prims);
             if (!src) {
                 fprintf(stderr, WO_LOG_PREFIX " scene specialisation: source generation failed; using the interpreter\n");
+            } else if (may_defer && !wo_dev_jit_cached(r->dev, src) && (r->jit_job = wo_jit_job_start(r->dev, src))) {
+                r->jit_want = src; /* compiling in the background; the interpreter meanwhile */
+                src = NULL;
+                deferred = 1;
             } else {
                 /* compiled once (code-object cache), loaded on every rank's device */
                 int ok = 1;
@@ -534,9 +607,12 @@ static int sync_device(Wo_Renderer* r) {
         if (!r->jit_loaded)
             for (uint32_t i = 0; i < r->ndevs; ++i) (void)wo_dev_set_jit(r->devs[i], NULL, err, sizeof err);
         if (cur >= 0) (void)wo_dev_select(cur);
+        (void)deferred;
     }
     return 0;
 }
+
+static int sync_device(Wo_Renderer* r) { return sync_device_ex(r, 0); }
 
 void wo_renderer_set_tracer(Wo_Renderer* r, Wo_Tracer tracer) {
     if (r->tracer != (int)tracer) {
@@ -729,7 +805,7 @@ void wo_renderer_draw_frame(Wo_Renderer* r) {
     if (!r) return;
     Wo_RenderParams p = r->draw;
     if (!r->pin_time) p.time_sec = (float)(r->app ? wo_app_time_sec(r->app) : wo_monotonic_sec() - r->t0);
-    if (sync_device(r)) {
+    if (sync_device_ex(r, r->jit_async)) {
         fprintf(stderr, WO_LOG_PREFIX " draw_frame failed: %s\n", wo_renderer_last_error());
         return;
     }
@@ -832,4 +908,8 @@ int wo_renderer_take_segments(Wo_Renderer* r, unsigned long long* total) {
     }
     if (cur >= 0) (void)wo_dev_select(cur);
     return rc;
+}
+
+void wo_renderer_set_jit_async(Wo_Renderer* r, int on) {
+    if (r) r->jit_async = on != 0;
 }

@@ -23,10 +23,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -309,6 +311,8 @@ constexpr uint32_t kNodeBound = 0u, kNodeSphere = 1u, kNodeGeneric = 2u;
 // bit.  A ray that starts inside some primitive (counted on the way: boxes that
 // contain the ray's start are never pruned) takes the general walk below.
 constexpr uint32_t kLeafRef = 0x80000000u, kNoRef = 0xffffffffu;
+// term mode (extract_terms): literals per term; a literal is ordinal | kLitNeg (complement)
+constexpr uint32_t kTermLits = 2, kLitNeg = 0x80000000u, kNoLit = 0xffffffffu;
 // The lane BVH is built with at most kLaneDepthMax internal levels on any path,
 // and the per-lane LDS stack holds as many entries as the built tree has levels:
 // a walk pushes at most one sibling per ancestor, so the stack never overflows.
@@ -334,12 +338,17 @@ __device__ __forceinline__ float box_near(float4 lo, float4 hi, F3 ri, F3 oi, fl
 
 // kMode: 0 general walk over the table in LDS, 1 general walk over the table in
 // global memory, 2 ordered BVH, 3 ordered BVH over single-sphere primitives only
-// (no generic-primitive code: fewer registers).
+// (no generic-primitive code: fewer registers); 4 / 5 = 2 / 3 with 16-bit stack
+// entries (trees of < 2^15 nodes and primitives: half the stacks' LDS, left to
+// top nodes); 6 ordered BVH over the terms of a root that is a union of small
+// conjunctions (extract_terms: the leaves and the always list hold terms).
 template <int kMode, bool kCountT>
 struct LaneTracer {
     static constexpr bool kCount = kCountT;
     static constexpr bool kBvh = kMode >= 2;
-    static constexpr bool kSpheresOnly = kMode == 3;
+    static constexpr bool kSpheresOnly = kMode == 3 || kMode == 5;
+    static constexpr bool kStack16 = kMode == 4 || kMode == 5;
+    static constexpr bool kTerms = kMode == 6;
     WorkCounts wk;
     uint64_t tmark;  // section timing (counting builds)
     const WoRec* __restrict__ prog;      // full program (generic primitives, hit leaves)
@@ -351,8 +360,10 @@ struct LaneTracer {
     const float4* __restrict__ lnodes;   // 4 float4 per node: childA lo|ref, childA hi|ref B, childB lo, childB hi
     const float4* __restrict__ lgeo;     // per ordinal: sphere centre, r^2 (single-sphere primitives)
     const uint32_t* __restrict__ lkind;  // per ordinal: 1 = single sphere, 0 = generic; then the always list
+    const uint2* __restrict__ lterms;    // term mode: a term's two literals (ordinal | kLitNeg, or kNoLit)
     uint32_t nalways, lroot, nprims;
     uint32_t* stk;                       // LDS stack column of this lane ([entry][lane])
+    uint16_t* stk16;                     // the same with 16-bit entries (kStack16): leaf bit 15
     // LDS copy of nodes [0, ntop) (the top levels, BFS order).  Typed by address
     // space so the two node reads of query() stay an LDS and a global load: one
     // pointer to either would be a flat load, which waits on both counters.
@@ -411,10 +422,62 @@ struct LaneTracer {
     // kEmptyKey; `inside` (first query only) counts the primitives whose
     // interval holds t_min.  Boxes are pruned beyond the best event so far; the
     // boxes holding the ray's start never are, so the count is complete.
-    __device__ __forceinline__ uint64_t query(F3 o, F3 d, F3 ri, F3 oi, uint64_t after, uint32_t& inside, F3& inv,
-                                              bool& have_inv) {
+    // `up`: the count of true members (primitives; terms in term mode) rises at
+    // the returned key.
+    __device__ __forceinline__ uint64_t query(F3 o, F3 d, F3 ri, F3 oi, uint64_t after, uint32_t& inside, bool& up,
+                                              F3& inv, bool& have_inv) {
         const float tmin = WO_T_MIN;
         uint64_t best = kEmptyKey;
+        bool best_up = false;
+        // Term mode: a term (a conjunction of one or two literals, each a primitive or
+        // its complement) changes value only at an event of a literal X, and then
+        // exactly when the other literal holds at that key; it rises where X's
+        // literal becomes true (X's entry for a positive literal, its exit for a
+        // complement).  A primitive is in one term, so one key changes one term.
+        auto visit_term = [&](uint32_t ti, uint32_t& cnt) {
+            const uint2 tl = lterms[ti];
+            uint64_t kin[2], kout[2];
+            bool valid[2], pos[2];
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                const uint32_t lit = x == 0 ? tl.x : tl.y;
+                kin[x] = 0ull;
+                kout[x] = kEmptyKey;
+                pos[x] = !(lit & kLitNeg);
+                valid[x] = false;
+                if (x == 1 && lit == kNoLit) continue;
+                const uint32_t ord = lit & ~kLitNeg;
+                const Ivl iv = prim_ivl(ord, o, d, inv, have_inv);
+                valid[x] = !(iv.a > iv.b) & (iv.b > tmin);
+                kin[x] = iv.a > tmin ? event_key(iv.a, ord, 0u, iv.ma) : 0ull;
+                kout[x] = iv.b < kInf ? event_key(iv.b, ord, 1u, iv.mb) : kEmptyKey;
+            }
+            const bool one = tl.y == kNoLit;
+            // the literal's value just around key e of the other literal (keys are distinct)
+            auto lit_at = [&](int x, uint64_t e) {
+                const bool in = valid[x] & (kin[x] < e) & (e < kout[x]);
+                return pos[x] ? in : !in;
+            };
+            const bool t0 = (pos[0] ? (valid[0] & (kin[0] == 0ull)) : !(valid[0] & (kin[0] == 0ull))) &
+                            (one | (pos[1] ? (valid[1] & (kin[1] == 0ull)) : !(valid[1] & (kin[1] == 0ull))));
+            if (t0) ++cnt;
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                const int y = 1 - x;
+                const bool has = valid[x] & !(x == 1 && one);
+                const uint64_t ei = kin[x], eo = kout[x];
+                if (has & (ei != 0ull) & (ei > after) & (ei < best) && (one | lit_at(y, ei))) {
+                    WO_WK(WO_WORK_EVENTS);
+                    best = ei;
+                    best_up = pos[x];
+                }
+                if (has & (eo != kEmptyKey) & (eo > after) & (eo < best) && (one | lit_at(y, eo))) {
+                    WO_WK(WO_WORK_EVENTS);
+                    best = eo;
+                    best_up = !pos[x];
+                }
+            }
+        };
         auto visit = [&](uint32_t ord, uint32_t& cnt) {
 #if WO_LANES_FUSED_SPHERE
             if constexpr (kSpheresOnly) {
@@ -459,12 +522,18 @@ struct LaneTracer {
                 }
             }
         };
+        auto leaf = [&](uint32_t ref, uint32_t& cnt) {
+            if constexpr (kTerms)
+                visit_term(ref, cnt);
+            else
+                visit(ref, cnt);
+        };
         uint32_t in_always = 0, in_tree = 0;
-        for (uint32_t i = 0; i < nalways; ++i) visit(lkind[nprims + i], in_always);
+        for (uint32_t i = 0; i < nalways; ++i) leaf(lkind[nprims + i], in_always);
         uint32_t cur = lroot, sp = 0;
         while (cur != kNoRef) {
             if (cur & kLeafRef) {
-                visit(cur & ~kLeafRef, in_tree);
+                leaf(cur & ~kLeafRef, in_tree);
                 cur = kNoRef;
             } else {
                 WO_WK_N(WO_WORK_BOUND_TESTS, 2u);
@@ -488,7 +557,10 @@ struct LaneTracer {
                     const bool a_first = na <= nb;
                     cur = a_first ? ra : rb;
                     const uint32_t other = a_first ? rb : ra;
-                    stk[sp * kBlock] = other;  // sp < the tree's depth (build_lbvh)
+                    if constexpr (kStack16)  // refs < 2^15 (build_lbvh): the leaf flag moves to bit 15
+                        stk16[sp * kBlock] = (uint16_t)((other & 0x7fffu) | ((other >> 16) & 0x8000u));
+                    else
+                        stk[sp * kBlock] = other;  // sp < the tree's depth (build_lbvh)
                     ++sp;
                 } else {
                     cur = ha ? ra : (hb ? rb : kNoRef);
@@ -496,10 +568,19 @@ struct LaneTracer {
             }
             if ((cur == kNoRef) & (sp != 0u)) {
                 --sp;
-                cur = stk[sp * kBlock];
+                if constexpr (kStack16) {
+                    const uint32_t e = stk16[sp * kBlock];
+                    cur = (e & 0x7fffu) | ((e & 0x8000u) << 16);
+                } else {
+                    cur = stk[sp * kBlock];
+                }
             }
         }
         inside = in_always + in_tree;
+        if constexpr (kTerms)
+            up = best_up;
+        else  // a primitive's count rises at its entry
+            up = !(best & kKeyTypeBit);
         return best;
     }
 
@@ -516,18 +597,19 @@ struct LaneTracer {
         F3 inv = f3(0.0f, 0.0f, 0.0f);
         bool have_inv = false;
         uint32_t cnt = 0, unused = 0;
-        uint64_t key = query(o, d, ri, oi, 0ull, cnt, inv, have_inv);
+        bool up = false;
+        uint64_t key = query(o, d, ri, oi, 0ull, cnt, up, inv, have_inv);
         const uint32_t root = cnt > 0u ? 1u : 0u;
         while (key != kEmptyKey) {
             WO_WK(WO_WORK_SWEEP_STEPS);
-            cnt = (key & kKeyTypeBit) ? cnt - 1u : cnt + 1u;
+            cnt = up ? cnt + 1u : cnt - 1u;
             const uint32_t rv = cnt > 0u ? 1u : 0u;
             if (rv != root) {
                 hit_from_key(key, rv, hit);
                 return true;
             }
             WO_WK(WO_WORK_RECOLLECTS);
-            key = query(o, d, ri, oi, key, unused, inv, have_inv);
+            key = query(o, d, ri, oi, key, unused, up, inv, have_inv);
         }
         return false;
     }
@@ -661,6 +743,7 @@ struct LaneBvh {
     const float4* nodes;
     const float4* geo;
     const uint32_t* kind;  // per ordinal, then the always list
+    const uint2* terms;    // term mode: two literals per term (ordinal | kLitNeg, or kNoLit)
     uint32_t nalways, root, nprims;
     uint32_t depth;        // internal levels of the tree: the lane stack's entries
     uint32_t ntop;         // nodes [0, ntop) staged in LDS after the lane stacks
@@ -672,7 +755,7 @@ struct LaneBvh {
 #define WO_LANES_BVH_MIN_WAVES 7  // rtiow_cover: 16.86 ms at 8, 16.63 at 7, 17.26 at 6
 #endif
 template <int kMode, bool kCount>
-__global__ __launch_bounds__(kBlock, kMode == 2 ? WO_LANES_BVH_MIN_WAVES : WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
+__global__ __launch_bounds__(kBlock, (kMode == 2 || kMode == 4 || kMode == 6) ? WO_LANES_BVH_MIN_WAVES : WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
     const WoRec* __restrict__ prog, const float4* __restrict__ gnodes, const uint32_t* __restrict__ ordpc,
     const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t ntrav, uint32_t local_rows, float4* __restrict__ out,
     unsigned long long* __restrict__ seg_slots, PathLaunch tg, LaneBvh bvh) {
@@ -685,16 +768,19 @@ __global__ __launch_bounds__(kBlock, kMode == 2 ? WO_LANES_BVH_MIN_WAVES : WO_LA
     tr.lnodes = bvh.nodes;
     tr.lgeo = bvh.geo;
     tr.lkind = bvh.kind;
+    tr.lterms = bvh.terms;
     tr.nalways = bvh.nalways;
     tr.lroot = bvh.root;
     tr.nprims = bvh.nprims;
     tr.stk = smem + threadIdx.x;  // kMode >= 2 only
+    tr.stk16 = reinterpret_cast<uint16_t*>(smem) + threadIdx.x;
     tr.ntop = 0;
     tr.ltop = (typename LaneTracer<kMode, kCount>::LdsNodes)nullptr;
     if constexpr (kMode >= 2) {
         // the top levels of the BVH next to the stacks; pathtrace_block's first
         // barrier orders the copy before any walk
-        float4* top = reinterpret_cast<float4*>(smem + bvh.depth * kBlock);
+        const uint32_t stack_words = (kMode >= 4 ? (bvh.depth * kBlock + 1u) / 2u : bvh.depth * kBlock);
+        float4* top = reinterpret_cast<float4*>(smem + ((stack_words + 3u) & ~3u));
         for (uint32_t i = threadIdx.x; i < 4u * bvh.ntop; i += kBlock) top[i] = bvh.nodes[i];
         tr.ltop = (typename LaneTracer<kMode, kCount>::LdsNodes)top;
         tr.ntop = bvh.ntop;
@@ -979,7 +1065,10 @@ struct WoDev {
     float4* d_lbvh;
     size_t lbvh_cap;
     uint32_t lb_nodes, lb_always, lb_root, lb_nprims;
-    bool lb_spheres_only;  // every primitive is a single sphere (kMode 3)
+    bool lb_spheres_only;  // every primitive is a single sphere (kMode 3 / 5)
+    bool lb_stack16;       // nodes and primitives < 2^15: 16-bit stack entries (kMode 4 / 5)
+    uint32_t lb_terms;     // term mode (kMode 6): terms the BVH's leaves and always list refer to
+    uint32_t lb_term_off;  // their literals (uint2 each) at this u32 offset of d_lbvh
     uint32_t lb_top;       // nodes staged in LDS per workgroup
     uint32_t lb_depth;     // internal levels of the lane BVH (<= kLaneDepthMax)
     unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
@@ -1154,7 +1243,26 @@ static int build_trav(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
             ++pc;
         }
     }
-    if (!union_only) return 0;
+    if (!union_only) {
+        // the term mode of the lane tracer (build_lbvh) reads primitives through
+        // the ordinal -> program pc map too
+        std::vector<uint32_t> ordpc(n_prims ? n_prims : 1u, 0u);
+        for (uint32_t pc = 0; pc < n_recs;) {
+            if (prog[pc].op == WO_OP_PRIM) {
+                if (prog[pc].u1 < n_prims) ordpc[prog[pc].u1] = pc;
+                pc += 1u + prog[pc].u0;
+            } else {
+                ++pc;
+            }
+        }
+        if (ensure_buffer(&dev->d_ordpc, &dev->ordpc_cap, ordpc.size() * sizeof(uint32_t), err, errlen)) return -1;
+        hipError_t e = hipMemcpy(dev->d_ordpc, ordpc.data(), ordpc.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            set_err(err, errlen, "hipMemcpy(ordinal map)", e);
+            return -1;
+        }
+        return 0;
+    }
     // pass 1: node index of every program record (binops and leaves map to the next node)
     std::vector<uint32_t> map(n_recs + 1u, 0u), ordpc(n_prims, 0u);
     uint32_t nn = 0;
@@ -1362,6 +1470,99 @@ static uint32_t lb_build(std::vector<LbPrim>& prims, uint32_t b, uint32_t e, uin
     return n;
 }
 
+// ---- union of conjunctions (the lane tracer's term mode) ----
+// A program whose root is a union of TERMS, each a conjunction of at most
+// kTermLits literals (a primitive or its complement: a DIFF of one primitive by
+// another is a AND NOT b) and each primitive in one term: csg256 / csg512
+// balanced's pairs, csg32's box minus sphere.  Along a ray, a term's value can
+// only change at an event of its own literals, so the root (a union) changes
+// exactly when the count of true terms crosses 0 -- the union-only sweep with
+// term transitions in place of primitive events (LaneTracer::visit_term).
+// Literal encoding: ordinal | kLitNeg for a complement.
+
+struct TermSub {
+    int kind;  // 0 conjunction (lits), 1 union of conjunctions (terms), 2 not expressible
+    std::vector<uint32_t> lits;
+    std::vector<std::vector<uint32_t>> terms;
+};
+
+// The root's terms, or false when the program is not such a union.
+static bool extract_terms(WoRec const* prog, uint32_t n_recs, uint32_t n_prims,
+                          std::vector<std::vector<uint32_t>>& terms) {
+    std::vector<TermSub> st;
+    auto bad = []() { TermSub t; t.kind = 2; return t; };
+    auto as_terms = [](const TermSub& x) {
+        return x.kind == 0 ? std::vector<std::vector<uint32_t>>{x.lits} : x.terms;
+    };
+    // NOT of a union of single positive literals (a difference's right operand)
+    auto negated = [](const TermSub& x, std::vector<uint32_t>& out) {
+        if (x.kind == 0) {
+            if (x.lits.size() != 1u || (x.lits[0] & kLitNeg)) return false;
+            out.push_back(x.lits[0] | kLitNeg);
+            return true;
+        }
+        if (x.kind != 1) return false;
+        for (const auto& t : x.terms) {
+            if (t.size() != 1u || (t[0] & kLitNeg)) return false;
+            out.push_back(t[0] | kLitNeg);
+        }
+        return true;
+    };
+    for (uint32_t pc = 0; pc < n_recs;) {
+        const WoRec& r = prog[pc];
+        if (r.op == WO_OP_PRIM) {
+            TermSub t;
+            t.kind = 0;
+            t.lits.push_back(r.u1);
+            st.push_back(t);
+            pc += 1u + r.u0;
+            continue;
+        }
+        ++pc;
+        if (r.op == WO_OP_BOUND) continue;  // a culling hint: evaluators may ignore it
+        if (st.size() < 2u) return false;
+        TermSub b = st.back();
+        st.pop_back();
+        TermSub a = st.back();
+        st.pop_back();
+        TermSub out = bad();
+        if (a.kind != 2 && b.kind != 2) {
+            if (r.op == WO_OP_UNION) {
+                out.kind = 1;
+                out.terms = as_terms(a);
+                const auto tb = as_terms(b);
+                out.terms.insert(out.terms.end(), tb.begin(), tb.end());
+            } else if (r.op == WO_OP_INTER && a.kind == 0 && b.kind == 0) {
+                out.kind = 0;
+                out.lits = a.lits;
+                out.lits.insert(out.lits.end(), b.lits.begin(), b.lits.end());
+            } else if ((r.op == WO_OP_DIFF || r.op == WO_OP_RDIFF)) {
+                const TermSub& keep = r.op == WO_OP_DIFF ? a : b;  // DIFF: a AND NOT b; RDIFF: b AND NOT a
+                const TermSub& sub = r.op == WO_OP_DIFF ? b : a;
+                std::vector<uint32_t> neg;
+                if (keep.kind == 0 && negated(sub, neg)) {
+                    out.kind = 0;
+                    out.lits = keep.lits;
+                    out.lits.insert(out.lits.end(), neg.begin(), neg.end());
+                }
+            }
+        }
+        st.push_back(out);
+    }
+    if (st.size() != 1u || st[0].kind == 2) return false;
+    terms = as_terms(st[0]);
+    std::vector<uint8_t> seen(n_prims, 0);
+    for (const auto& t : terms) {
+        if (t.empty() || t.size() > kTermLits) return false;
+        for (uint32_t l : t) {
+            const uint32_t o = l & ~kLitNeg;
+            if (o >= n_prims || seen[o]) return false;  // one term per primitive
+            seen[o] = 1;
+        }
+    }
+    return true;
+}
+
 // Union-only programs: an AABB BVH over the bounded primitives (boxes expanded by
 // 1e-4 of their size and position plus 1e-5, so the approximate slab test never
 // culls a primitive the exact arithmetic meets) and the always list: unbounded
@@ -1373,12 +1574,22 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     dev->lb_root = kNoRef;
     dev->lb_nprims = n_prims;
     dev->lb_spheres_only = false;
+    dev->lb_stack16 = false;
+    dev->lb_terms = 0;
     const char* env = getenv("WOLOLO_LANES_BVH");
-    if (!dev->union_only || (env && env[0] == '0')) return 0;
+    if (env && env[0] == '0') return 0;
+    // not union-only: the BVH over the root's terms, when the root is a union of
+    // small conjunctions (extract_terms)
+    std::vector<std::vector<uint32_t>> terms;
+    if (!dev->union_only) {
+        const char* tv = getenv("WOLOLO_LANES_TERMS");
+        if ((tv && tv[0] == '0') || !extract_terms(prog, n_recs, n_prims, terms)) return 0;
+    }
     std::vector<LbPrim> prims;
     std::vector<uint32_t> always;
     std::vector<float4> geo(n_prims, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     std::vector<uint32_t> kind(n_prims, 0u);
+    std::vector<uint32_t> pc_of(n_prims, 0u);
     for (uint32_t pc = 0; pc < n_recs;) {
         const WoRec& r = prog[pc];
         if (r.op != WO_OP_PRIM) {
@@ -1395,6 +1606,11 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
             geo[ord] = make_float4(L.f[0], L.f[1], L.f[2], L.f[3]);
             kind[ord] = 1u;
         }
+        pc_of[ord] = pc;
+        if (!terms.empty()) {  // boxes per term below
+            pc += 1u + r.u0;
+            continue;
+        }
         LbPrim p;
         p.ord = ord;
         if (prim_aabb(prog, pc, p.lo, p.hi)) {
@@ -1409,6 +1625,45 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
             always.push_back(ord);
         }
         pc += 1u + r.u0;
+    }
+    // term mode: a term's box is the meet of its positive literals' boxes (its
+    // value, and every change of it, lies inside each of them); a term with no
+    // bounded positive literal goes to the always list
+    std::vector<uint2> term_lits;
+    for (uint32_t ti = 0; ti < (uint32_t)terms.size(); ++ti) {
+        const auto& t = terms[ti];
+        uint2 tl = make_uint2(t[0], t.size() > 1u ? t[1] : kNoLit);
+        term_lits.push_back(tl);
+        LbPrim p;
+        p.ord = ti;
+        bool bounded = false;
+        for (int a = 0; a < 3; ++a) {
+            p.lo[a] = -INFINITY;
+            p.hi[a] = INFINITY;
+        }
+        for (uint32_t l : t) {
+            if (l & kLitNeg) continue;
+            double lo[3], hi[3];
+            if (!prim_aabb(prog, pc_of[l], lo, hi)) continue;
+            bounded = true;
+            for (int a = 0; a < 3; ++a) {
+                p.lo[a] = fmax(p.lo[a], lo[a]);
+                p.hi[a] = fmin(p.hi[a], hi[a]);
+            }
+        }
+        for (int a = 0; a < 3 && bounded; ++a)
+            if (p.lo[a] > p.hi[a]) p.hi[a] = p.lo[a];  // an empty meet: a point box (never empty arithmetic)
+        if (!bounded) {
+            always.push_back(ti);
+            continue;
+        }
+        for (int a = 0; a < 3; ++a) {
+            const double m = 1e-4 * (fabs(p.lo[a]) + fabs(p.hi[a]) + (p.hi[a] - p.lo[a])) + 1e-5;
+            p.lo[a] -= m;
+            p.hi[a] += m;
+            p.c[a] = 0.5 * (p.lo[a] + p.hi[a]);
+        }
+        prims.push_back(p);
     }
     if (!prims.empty()) {
         std::vector<double> diag(prims.size());
@@ -1474,16 +1729,26 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     dev->lb_nodes = (uint32_t)(nodes.size() / 4u);
     dev->lb_always = (uint32_t)always.size();
     {
+        // 16-bit stack entries when every ref fits 15 bits (WOLOLO_LANES_STACK16=0: 32-bit)
+        const char* s16 = getenv("WOLOLO_LANES_STACK16");
+        dev->lb_stack16 = terms.empty() && dev->lb_nodes < 0x8000u && n_prims < 0x8000u && s16 && s16[0] == '1';
         // the top nodes fill what the stacks leave of kLanesBvhLds (8 workgroups per CU)
-        const size_t stacks = (size_t)dev->lb_depth * kBlock * sizeof(uint32_t);
+        const size_t stacks =
+            ((((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u)) + 15u) & ~(size_t)15u);
         uint32_t top = stacks < kLanesBvhLds ? (uint32_t)((kLanesBvhLds - stacks) / (4u * sizeof(float4))) : 0u;
         const char* v = getenv("WOLOLO_LANES_TOP");
         if (v && *v) top = (uint32_t)strtoul(v, NULL, 10);
         dev->lb_top = top < dev->lb_nodes ? top : dev->lb_nodes;
     }
-    dev->lb_spheres_only = std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
+    dev->lb_spheres_only = terms.empty() && std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
+    dev->lb_terms = (uint32_t)terms.size();
     const size_t f4 = nodes.size() + n_prims;
-    const size_t bytes = f4 * sizeof(float4) + ((size_t)n_prims + always.size()) * sizeof(uint32_t);
+    // ... | kind per ordinal | always list | (term mode) uint2 literals per term, 8-byte aligned
+    size_t words = (size_t)n_prims + always.size();
+    words = (words + 1u) & ~(size_t)1u;
+    const size_t term_off = f4 * sizeof(float4) + words * sizeof(uint32_t);
+    dev->lb_term_off = (uint32_t)(term_off / sizeof(uint32_t));
+    const size_t bytes = term_off + term_lits.size() * sizeof(uint2);
     if (ensure_buffer(&dev->d_lbvh, &dev->lbvh_cap, bytes, err, errlen)) return -1;
     std::vector<char> blob(bytes);
     memcpy(blob.data(), nodes.data(), nodes.size() * sizeof(float4));
@@ -1491,6 +1756,7 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     memcpy(blob.data() + f4 * sizeof(float4), kind.data(), n_prims * sizeof(uint32_t));
     memcpy(blob.data() + f4 * sizeof(float4) + n_prims * sizeof(uint32_t), always.data(),
            always.size() * sizeof(uint32_t));
+    if (!term_lits.empty()) memcpy(blob.data() + term_off, term_lits.data(), term_lits.size() * sizeof(uint2));
     hipError_t e = hipMemcpy(dev->d_lbvh, blob.data(), bytes, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         set_err(err, errlen, "hipMemcpy(lane BVH)", e);
@@ -1509,6 +1775,9 @@ static LaneBvh lane_bvh(const WoDev* dev) {
     b.nprims = dev->lb_nprims;
     b.ntop = dev->lb_top;
     b.depth = dev->lb_depth;
+    b.terms = dev->lb_terms ? reinterpret_cast<const uint2*>(reinterpret_cast<const uint32_t*>(dev->d_lbvh) +
+                                                            dev->lb_term_off)
+                            : nullptr;
     return b;
 }
 
@@ -1773,6 +2042,64 @@ extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t err
     return 0;
 }
 
+// ---- background compiles (wo_dev.h WoJitJob) ----
+extern "C" int wo_dev_jit_cached(WoDev* dev, const char* src) {
+    const std::string key = jit_key(src, dev->arch);
+    {
+        std::lock_guard<std::mutex> lock(g_jit_mu);
+        if (jit_cache().count(key)) return 1;
+    }
+    void* buf = nullptr;
+    size_t n = 0;
+    if (wo_jit_disk_load(key.c_str(), &buf, &n) != 0) return 0;
+    std::vector<char> code((char*)buf, (char*)buf + n);
+    free(buf);
+    std::lock_guard<std::mutex> lock(g_jit_mu);
+    jit_cache_put(key, code);
+    return 1;
+}
+
+struct WoJitJob {
+    std::thread th;
+    std::atomic<int> done{0};
+    int rc = 0;
+    std::string src, arch;
+    char err[512] = {0};
+};
+
+extern "C" WoJitJob* wo_jit_job_start(WoDev* dev, const char* src) {
+    WoJitJob* j = new (std::nothrow) WoJitJob();
+    if (!j) return nullptr;
+    j->src = src;
+    j->arch = dev->arch;
+    try {
+        j->th = std::thread([j]() {
+            std::vector<char> code;
+            std::string key;
+            int origin = -1;
+            double sec = 0.0;
+            j->rc = jit_code(j->src.c_str(), j->arch, false, code, key, origin, sec, j->err, sizeof j->err);
+            j->done.store(1, std::memory_order_release);
+        });
+    } catch (...) {
+        delete j;
+        return nullptr;
+    }
+    return j;
+}
+
+extern "C" int wo_jit_job_done(WoJitJob* j) { return j->done.load(std::memory_order_acquire); }
+
+extern "C" const char* wo_jit_job_source(WoJitJob* j) { return j->src.c_str(); }
+
+extern "C" int wo_jit_job_finish(WoJitJob* j, char* err, size_t errlen) {
+    if (j->th.joinable()) j->th.join();
+    const int rc = j->rc;
+    if (rc && err && errlen) snprintf(err, errlen, "%s", j->err);
+    delete j;
+    return rc;
+}
+
 extern "C" int wo_dev_jit_origin(WoDev* dev, double* seconds) {
     if (!dev || !dev->jit_fn) return -1;
     if (seconds) *seconds = dev->jit_compile_sec;
@@ -1794,7 +2121,9 @@ extern "C" int wo_jit_compile_check(const char* src, const char* arch, char* err
 }
 
 extern "C" int wo_dev_jit_active(WoDev* dev) { return dev && dev->jit_fn ? 1 : 0; }
-extern "C" int wo_dev_lanes_available(WoDev* dev) { return dev && dev->union_only ? 1 : 0; }
+extern "C" int wo_dev_lanes_available(WoDev* dev) {
+    return dev && (dev->union_only || dev->lb_terms) ? 1 : 0;
+}
 extern "C" void wo_dev_set_lanes(WoDev* dev, int on) {
     if (dev) dev->lanes_on = on != 0;
 }
@@ -1880,7 +2209,8 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
     return wo_dev_launch_ex(dev, frame_in, d_out, stream_v, d_segments, nullptr, 0u, err, errlen);
 }
 
-enum PathKind { kLanesLds, kLanesGlobal, kLanesBvh, kLanesBvhSpheres, kJit, kInterpLds, kInterpGlobal };
+enum PathKind { kLanesLds, kLanesGlobal, kLanesBvh, kLanesBvhSpheres, kLanesBvh16, kLanesBvhSpheres16, kLanesTerms, kJit,
+                kInterpLds, kInterpGlobal };
 
 template <bool kCount>
 static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
@@ -1893,6 +2223,12 @@ static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<2, kCount>, kBlock, dyn_lds);
     case kLanesBvhSpheres:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<3, kCount>, kBlock, dyn_lds);
+    case kLanesBvh16:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<4, kCount>, kBlock, dyn_lds);
+    case kLanesBvhSpheres16:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<5, kCount>, kBlock, dyn_lds);
+    case kLanesTerms:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<6, kCount>, kBlock, dyn_lds);
     case kInterpLds:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_kernel<true, kCount>, kBlock, dyn_lds);
     default:
@@ -1922,6 +2258,21 @@ static void static_launch(PathKind kind, dim3 grid, size_t dyn_lds, hipStream_t 
         break;
     case kLanesBvhSpheres:
         hipLaunchKernelGGL((pathtrace_lanes_kernel<3, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesBvh16:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<4, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesBvhSpheres16:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<5, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesTerms:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<6, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
                            dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
                            lane_bvh(dev));
         break;
@@ -1998,13 +2349,16 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
         PathKind kind;
         size_t dyn_lds = 0;
         KLayout lay = {};
-        if (dev->lanes_on && dev->union_only && !dev->jit_fn) {
+        if (dev->lanes_on && (dev->union_only || dev->lb_terms) && !dev->jit_fn) {
             // the ordered BVH: the lane stacks in LDS; the general walk: its table
             // in LDS when it fits
             const size_t table = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
             if (dev->lb_root != kNoRef || dev->lb_always != 0u) {
-                kind = dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh;
-                dyn_lds = (size_t)dev->lb_depth * kBlock * sizeof(uint32_t) + (size_t)dev->lb_top * 4u * sizeof(float4);
+                kind = dev->lb_terms   ? kLanesTerms
+                       : dev->lb_stack16 ? (dev->lb_spheres_only ? kLanesBvhSpheres16 : kLanesBvh16)
+                                         : (dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh);
+                const size_t stacks = ((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u) + 15u) & ~(size_t)15u;
+                dyn_lds = stacks + (size_t)dev->lb_top * 4u * sizeof(float4);
             } else {
                 kind = table <= kLanesLdsBudget ? kLanesLds : kLanesGlobal;
                 dyn_lds = kind == kLanesLds ? table : 0u;

@@ -47,6 +47,18 @@ int wo_dev_upload_scene(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t
  * NORMALS frames launch it instead of the interpreter kernel. */
 int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t errlen);
 int wo_dev_jit_active(WoDev* dev);
+/* 1 when the code object of `src` for the device's target is in this process's
+ * cache or the disk cache (then loading it takes milliseconds), else 0. */
+int wo_dev_jit_cached(WoDev* dev, const char* src);
+/* A compile of `src` for dev's target on a background host thread, into the
+ * process cache (and the disk cache): wo_dev_set_jit then loads it at once.
+ * done: 1 once the compile has ended; finish joins the thread and frees the job
+ * (0, or -1 with the compiler's message). */
+typedef struct WoJitJob WoJitJob;
+WoJitJob* wo_jit_job_start(WoDev* dev, const char* src);
+int wo_jit_job_done(WoJitJob* job);
+const char* wo_jit_job_source(WoJitJob* job);
+int wo_jit_job_finish(WoJitJob* job, char* err, size_t errlen);
 /* Lane traversal kernel (union-only programs, see trace_kernels.hip). */
 int wo_dev_lanes_available(WoDev* dev);
 void wo_dev_set_lanes(WoDev* dev, int on);

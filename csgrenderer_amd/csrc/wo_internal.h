@@ -74,6 +74,12 @@ struct Wo_Renderer {
 
     int tracer;         /* Wo_Tracer */
     int jit_loaded;     /* the device runs the scene-specialised kernel */
+    /* background compile (draw_frame): frames use the interpreter until it ends */
+    WoJitJob* jit_job;      /* compiling jit_want */
+    char* jit_want;         /* the current scene's specialised source, while deferred */
+    WoJitJob* jit_old[8];   /* compiles of scenes edited since (joined when done) */
+    uint32_t n_jit_old;
+    int jit_async;          /* draw_frame may defer the compile (default; WOLOLO_JIT_ASYNC=0: off) */
     int lanes_loaded;   /* the device runs the lane-traversal kernel */
 
     uint64_t frames_drawn;

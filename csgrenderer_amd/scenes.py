@@ -329,7 +329,7 @@ def build_csg32_nested(r: Renderer, seed: int = 3235, width=1920, height=1080, s
 
 
 def build_csg256(r: Renderer, seed: int = 256, shape: str = "balanced", width=1920, height=1080,
-                 spp=64, union_only=False) -> SceneInfo:
+                 spp=64, union_only=False, pairs: int = 63) -> SceneInfo:
     """C5: 128 sphere leaves, 127 binops (255 nodes), leaf 0 an RTIOW-style ground
     sphere (r = 1000).
       balanced: 63 overlapping pairs (ops cycle u/d/i) + ground + 1 sphere, joined
@@ -341,7 +341,7 @@ def build_csg256(r: Renderer, seed: int = 256, shape: str = "balanced", width=19
     r.set_material(ground, r.lambertian((0.5, 0.5, 0.5)))
     gitem = (ground, (0.0, -1000.0, 0.0))
     if shape == "balanced":
-        items = [gitem] + _overlapping_pairs(r, rng, 63, (-5.0, 0.3, -5.0), (5.0, 2.5, 5.0), 0.25, 0.6,
+        items = [gitem] + _overlapping_pairs(r, rng, pairs, (-5.0, 0.3, -5.0), (5.0, 2.5, 5.0), 0.25, 0.6,
                                                _cycle("uui" if union_only else "udi"))
         s = r.sphere(1.0)
         r.set_material(s, r.dielectric(1.5))
@@ -361,8 +361,10 @@ def build_csg256(r: Renderer, seed: int = 256, shape: str = "balanced", width=19
     else:
         raise ValueError(shape)
     r.set_camera((0.0, 6.0, 13.0), (0.0, 0.8, 0.0), (0, 1, 0), 45.0, 0.0, 13.0)
-    return SceneInfo(f"csg256_{shape}" + ("_union" if union_only else ""), spheres=128, halfspaces=0, binops=127, width=width, height=height, spp=spp,
-                     max_depth=8)
+    leaves = 2 * pairs + 2 if shape == "balanced" else 128
+    name = f"csg256_{shape}" if leaves == 128 else f"csg{leaves}_{shape}"
+    return SceneInfo(name + ("_union" if union_only else ""), spheres=leaves, halfspaces=0, binops=leaves - 1, width=width,
+                     height=height, spp=spp, max_depth=8)
 
 
 SCENES = {
@@ -375,6 +377,10 @@ SCENES = {
     "csg256_balanced_union": lambda r, **k: build_csg256(r, shape="balanced", union_only=True, **k),
     "csg256_balanced": lambda r, **k: build_csg256(r, shape="balanced", **k),
     "csg256_chain": lambda r, **k: build_csg256(r, shape="chain", **k),
+    # more than WOLOLO_JIT_MAX_PRIMS primitives and not union-only: the interpreter's
+    # scene (512 sphere leaves: 255 overlapping pairs + ground + glass ball, 427
+    # primitives) -- not a BASELINE config, the measure of the >256-primitive path
+    "csg512_balanced": lambda r, **k: build_csg256(r, shape="balanced", pairs=255, **k),
 }
 
 

@@ -136,6 +136,8 @@ SIGNATURES = {
     "wo_renderer_set_jit": (None, [c_void_p, c_int]),
     "wo_renderer_set_tracer": (None, [c_void_p, c_int]),
     "wo_renderer_trace_path": (c_char_p, [c_void_p]),
+    "wo_renderer_set_jit_async": (None, [c_void_p, c_int]),
+    "wo_renderer_jit_pending": (c_int, [c_void_p]),
     "wo_renderer_jit_source": (c_void_p, [c_void_p]),
     "wo_jit_compile_check": (c_int, [c_char_p, c_char_p, c_char_p, c_size_t]),
     "wo_jit_code_object": (ctypes.c_longlong, [c_char_p, c_char_p, POINTER(c_int), POINTER(c_double), c_char_p,
@@ -320,6 +322,12 @@ class Renderer:
         if isinstance(tracer, str):
             tracer = TRACERS[tracer]
         self.lib.wo_renderer_set_tracer(self.ptr, int(tracer))
+
+    def set_jit_async(self, on: bool):
+        self.lib.wo_renderer_set_jit_async(self.ptr, 1 if on else 0)
+
+    def jit_pending(self) -> bool:
+        return bool(self.lib.wo_renderer_jit_pending(self.ptr))
 
     def trace_path(self) -> str:
         return self.lib.wo_renderer_trace_path(self.ptr).decode()

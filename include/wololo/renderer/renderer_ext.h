@@ -206,6 +206,17 @@ void wo_renderer_set_tracer(Wo_Renderer* r, Wo_Tracer tracer);
 void wo_renderer_set_jit(Wo_Renderer* r, int mode);
 /* Which path kernel the last render used: "jit", "lanes", "interpreter" or "none". */
 char const* wo_renderer_trace_path(Wo_Renderer* r);
+/* Scene edits do not stall draw_frame (on by default; WOLOLO_JIT_ASYNC=0 turns it
+ * off): when the specialised kernel of the edited scene is in neither code-object
+ * cache, draw_frame starts its hiprtc compile on a background host thread and
+ * renders with the interpreter -- the same image bit for bit -- until the compile
+ * has ended; the first draw_frame after that switches to it.  render_f32,
+ * render_accumulate, render_rows_device, render_frame_device and count_work wait
+ * for a compile in flight (batch renders get the specialised kernel).  The
+ * nodes are added incrementally as in the reference (renderer.c:2232-2275). */
+void wo_renderer_set_jit_async(Wo_Renderer* r, int on);
+/* 1 while a background compile of the current scene's kernel is in flight. */
+int wo_renderer_jit_pending(Wo_Renderer* r);
 
 /* HIP source of the scene-specialised kernel for the current scene (NULL if
  * the scene has no primitives); release with wo_free(). */

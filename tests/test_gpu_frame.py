@@ -377,3 +377,48 @@ def test_auto_rank_rule_keeps_the_reference_shader_on_one_device(monkeypatch):
     print(f"demo 1280x720 draw_frame: auto (1 rank) {auto_ms:.3f} ms, 8 stacked ranks {eight_ms:.3f} ms")
     assert auto_ms < eight_ms
     r.close()
+
+
+def test_scene_edit_does_not_stall_draw_frame():
+    """a node added between two draw_frame calls used to stall the
+    second for the specialised kernel's compile (~4 s for csg256).  Now draw_frame
+    starts the compile on a host thread and renders with the interpreter (the same
+    image bit for bit) meanwhile; a batch render waits for it and gets the kernel."""
+    import time
+    r = wl.Renderer("async-edit", max_nodes=4096)
+    info = scenes.build("csg256_balanced", r)
+    p = info.params(width=96, height=54, spp=2, seed=3)
+    r.set_draw_params(p)
+    r.render(p)
+    assert r.trace_path() == "jit"
+    r.draw_frame()
+    r.finish()
+    # an edit no code-object cache has seen: spheres at a random offset
+    off = 0.5 + (int.from_bytes(os.urandom(4), "little") % 100000) / 400000.0
+    r.union(wl.arg(r.sphere(0.3), (off, 1.0, 2.0)), wl.arg(r.sphere(0.2), (0.0, 1.5, 2.5)))
+    wl.clear_error()
+    t0 = time.perf_counter()
+    r.draw_frame()
+    dt = time.perf_counter() - t0
+    assert dt < 0.1, f"draw_frame after a scene edit took {dt * 1e3:.1f} ms"
+    assert r.jit_pending() and r.trace_path() == "interpreter"
+    r.draw_frame()  # more frames while the compile runs
+    r.finish()
+    during = r.last_frame()
+    after = r.render(p)  # waits for the compile
+    assert r.trace_path() == "jit" and not r.jit_pending()
+    _cmp(during, after, "frame rendered while the kernel compiled")
+    r.draw_frame()
+    r.finish()
+    _cmp(r.last_frame(), after, "first draw_frame on the new kernel")
+    # an edit before the previous compile ends: that compile is orphaned, not waited for
+    r.union(wl.arg(r.sphere(0.25), (off, 0.7, 1.5)), wl.arg(r.sphere(0.2), (-off, 0.7, 1.5)))
+    r.draw_frame()
+    r.union(wl.arg(r.sphere(0.15), (off, 0.4, 1.0)), wl.arg(r.sphere(0.1), (-off, 0.4, 1.0)))
+    t0 = time.perf_counter()
+    r.draw_frame()
+    assert time.perf_counter() - t0 < 0.1
+    r.finish()
+    _cmp(r.last_frame(), r.render(p), "two quick edits")
+    assert wl.last_error() == ""
+    r.close()

@@ -92,15 +92,56 @@ def _union_only(r):
     return nprim > 0
 
 
+def _union_of_terms(r, max_lits=2):
+    """Restatement of trace_kernels.hip extract_terms: the root is a union of terms, each
+    a conjunction of at most max_lits literals (a primitive or its complement), and
+    every primitive is in one term -- the lane tracer's term mode."""
+    prog, nrec, nprim = r.program()
+    st = []
+    pc = 0
+    while pc < nrec:
+        op = prog[pc].op
+        if op == wl.WO_OP_PRIM:
+            st.append(("conj", [(prog[pc].u1, True)]))
+            pc += 1 + prog[pc].u0
+            continue
+        pc += 1
+        if op == wl.WO_OP_BOUND:
+            continue
+        b, a = st.pop(), st.pop()
+        out = ("bad", None)
+        terms_of = lambda x: [x[1]] if x[0] == "conj" else x[1]
+        if a[0] != "bad" and b[0] != "bad":
+            if op == wl.WO_OP_UNION:
+                out = ("union", terms_of(a) + terms_of(b))
+            elif op == wl.WO_OP_INTER and a[0] == b[0] == "conj":
+                out = ("conj", a[1] + b[1])
+            elif op in (wl.WO_OP_DIFF, wl.WO_OP_RDIFF):
+                keep, sub = (a, b) if op == wl.WO_OP_DIFF else (b, a)
+                singles = terms_of(sub)
+                if keep[0] == "conj" and all(len(t) == 1 and t[0][1] for t in singles):
+                    out = ("conj", keep[1] + [(t[0][0], False) for t in singles])
+        st.append(out)
+    if len(st) != 1 or st[0][0] == "bad":
+        return False
+    terms = [st[0][1]] if st[0][0] == "conj" else st[0][1]
+    ords = [o for t in terms for o, _ in t]
+    return all(1 <= len(t) <= max_lits for t in terms) and len(ords) == len(set(ords))
+
+
+def _lanes_eligible(r):
+    return _union_only(r) or _union_of_terms(r)
+
+
 def _check_path(r, path, scene=None):
     """The kernel the tracer setting must have selected (renderer_ext.h Wo_Tracer)."""
     nprim = r.program()[2]
     if path == "interpreter":
         want = "interpreter"
-    elif path == "lanes" and _union_only(r):
+    elif path == "lanes" and _lanes_eligible(r):
         want = "lanes"
     else:  # JIT up to WOLOLO_JIT_MAX_PRIMS (256) primitives, e.g. rtiow_cover's 487 stay interpreted
-        want = "jit" if 0 < nprim <= 256 else "interpreter"
+        want = "jit" if 0 < nprim <= 256 else ("lanes" if _lanes_eligible(r) else "interpreter")
     assert r.trace_path() == want, (scene, r.trace_path(), want)
 
 
@@ -132,9 +173,9 @@ def test_pathtrace_full_size_sampled_pixels(scene, path):
     the GPU, a random sample of pixels on the oracle.  The lane tracer runs union-only
     scenes only (elsewhere the setting falls back to the JIT, which its own case covers)."""
     r, info = _scene(scene, path)
-    if path == "lanes" and not _union_only(r):
+    if path == "lanes" and not _lanes_eligible(r):
         r.close()
-        pytest.skip("lanes: not a union-only scene (the tracer falls back to the jit case)")
+        pytest.skip("lanes: not a union of small terms (the tracer falls back to the jit case)")
     p = info.params()
     img = r.render(p)
     _check_path(r, path, scene)
@@ -380,10 +421,14 @@ def _union_scene(n_spheres=90):
     return r
 
 
+@pytest.mark.parametrize("stack16", [None, "1"])
 @pytest.mark.parametrize("tracer", ["lanes", "auto"])
-def test_lanes_union_scene_bitexact(tracer, monkeypatch):
-    # AUTO takes the lane tracer for union-only scenes above WOLOLO_LANES_MIN_PRIMS (256 by default)
+def test_lanes_union_scene_bitexact(tracer, stack16, monkeypatch):
+    # AUTO takes the lane tracer for union-only scenes above WOLOLO_LANES_MIN_PRIMS (256 by default);
+    # the BVH walk's stack has 32-bit entries by default, 16-bit ones with WOLOLO_LANES_STACK16=1
     monkeypatch.setenv("WOLOLO_LANES_MIN_PRIMS", "64")
+    if stack16 is not None:
+        monkeypatch.setenv("WOLOLO_LANES_STACK16", stack16)
     r = _union_scene()
     assert _union_only(r) and r.program()[2] > 64
     r.set_tracer(tracer)
