@@ -96,6 +96,7 @@ typedef struct Gen {
     int first_event;  /* the first event of waves that start outside every primitive from a constant table */
     int fused_sphere; /* a lone sphere's membership and events inside its sqrt branch (no empty interval) */
     int dl_eval;      /* chains of literal sets evaluated as decision lists (gen_eval_flat) */
+    int term_mode;    /* root a union of <= 2-literal conjunctions: term transitions, no event window (gen_term) */
     int union_count;  /* root a union of literal sets: a count of true terms kept per event */
     int spatial;      /* collect grouped by a spatial hierarchy over the primitives (gen_spatial) */
     int spatial_sah;  /* its splits by least surface area instead of at the median */
@@ -103,6 +104,8 @@ typedef struct Gen {
     double spatial_ct;     /* group-test cost for SAH leaf decisions (0: split down to spatial_leaf) */
     struct SPrim* sprims;  /* the bounded primitives it groups */
     uint32_t nsprims;
+    struct SPrim* tunb;    /* term mode: terms without a bounding sphere (tested first, ungrouped) */
+    uint32_t ntunb;
     struct DList* dls; /* decision-list pool (ids are 1-based; 0 = none) */
     uint32_t ndl, dl_cap;
     int err;
@@ -123,6 +126,98 @@ static int bound_tested(const Gen* g, uint32_t pc) {
 
 /* ---- collect: intersect every primitive of [start, end), fill the window ---- */
 static void gen_lone_sphere(Gen* g, const WoRec* L, uint32_t ord, int indent);
+
+/* The members of the convex primitive at pc (cnt leaves) met into `iv`
+ * (declared by the caller with `float la, lb;`): the wave-level member skip,
+ * fused slab face pairs, literal constants. */
+static void gen_members(Gen* g, uint32_t pc, uint32_t cnt, int indent) {
+    static const char* nl[4] = {"c0", "c1", "c2", "c3"};
+    int open_skips = 0;
+    for (uint32_t m = 0; m < cnt; ++m) {
+        const WoRec* L = &g->prog[pc + 1 + m];
+        uint32_t vl[4];
+        for (int i = 0; i < 4; ++i) vl[i] = fbits(L->f[i]);
+        if (m > 0 && g->member_skip) /* empty on every lane: the other members cannot widen it */
+            bput(g->b, "%*s  if (__ballot(!(iv.a > iv.b)) != 0ull) {\n", indent, ""), ++open_skips;
+        bput(g->b, "%*s  {\n", indent, "");
+        const WoRec* L2 = m + 1u < cnt ? &g->prog[pc + 2 + m] : NULL;
+        if (g->axis_pairs && L->op == WO_LEAF_HALFSPACE && L->u1 != 0u && L2 && L2->op == WO_LEAF_HALFSPACE &&
+            L2->u1 == L->u1 && (L->f[L->u1 - 1u] > 0.0f) != (L2->f[L2->u1 - 1u] > 0.0f)) {
+            /* two faces of a slab: one entry, one exit (axis_pair_meet) */
+            static const char* nh[2] = {"c3", "c3b"};
+            static const char axis[3] = {'x', 'y', 'z'};
+            const char ax = axis[L->u1 - 1u];
+            const int pos = L->f[L->u1 - 1u] > 0.0f; /* s1 = +1 */
+            uint32_t vh[2] = {vl[3], fbits(L2->f[3])};
+            bput(g->b, "%*s    WO_WK_N(WO_WORK_HALFSPACE_TESTS, 2u);\n", indent, "");
+            if (m == 0) bput(g->b, "%*s    wodev::ivl_open(iv);\n", indent, "");
+            if (g->lit_consts) {
+                /* dist1 = h1 - s1*oa, dist2 = h2 + s1*oa with h as a literal operand */
+                bput(g->b,
+                     "%*s    float dist1, dist2;\n"
+                     "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist1) : \"v\"(o.%c));\n"
+                     "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist2) : \"v\"(o.%c));\n"
+                     "%*s    wodev::axis_pair_meet_d(iv, %s, dist1, dist2, d.%c, iv%c, %uu, %uu);\n%*s  }\n",
+                     indent, "", indent, "", pos ? "v_sub_f32_e32" : "v_add_f32_e32", vh[0], ax, indent, "",
+                     pos ? "v_add_f32_e32" : "v_sub_f32_e32", vh[1], ax, indent, "", pos ? "1.0f" : "-1.0f", ax,
+                     ax, m, m + 1u, indent, "");
+            } else {
+                emit_consts(g->b, indent + 4, "float", nh, vh, 2);
+                bput(g->b,
+                     "%*s    wodev::axis_pair_meet(iv, %s, c3, c3b, o.%c, d.%c, iv%c, %uu, %uu);\n%*s  }\n",
+                     indent, "", pos ? "1.0f" : "-1.0f", ax, ax, ax, m, m + 1u, indent, "");
+            }
+            ++m;
+            continue;
+        }
+        bput(g->b, "%*s    WO_WK(%s);\n", indent, "",
+             L->op == WO_LEAF_SPHERE ? "WO_WORK_SPHERE_TESTS" : "WO_WORK_HALFSPACE_TESTS");
+        if (L->op == WO_LEAF_HALFSPACE && L->u1 != 0u) {
+            /* axis-aligned: s = +-1 stays a literal (inline constant), h in an SGPR */
+            static const char* nh[1] = {"c3"};
+            static const char axis[3] = {'x', 'y', 'z'};
+            char ax = axis[L->u1 - 1u];
+            const int pos = L->f[L->u1 - 1u] > 0.0f;
+            if (g->lit_consts) {
+                bput(g->b,
+                     "%*s    float dist;\n"
+                     "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist) : \"v\"(o.%c));\n"
+                     "%*s    wodev::halfspace_axis_dist(%s, dist, d.%c, iv%c, la, lb);\n",
+                     indent, "", indent, "", pos ? "v_sub_f32_e32" : "v_add_f32_e32", vl[3], ax, indent, "",
+                     pos ? "1.0f" : "-1.0f", ax, ax);
+            } else {
+                emit_consts(g->b, indent + 4, "float", nh, &vl[3], 1);
+                bput(g->b,
+                     "%*s    wodev::halfspace_axis_interval(%s, c3, o.%c, d.%c, iv%c, la, lb);\n",
+                     indent, "", pos ? "1.0f" : "-1.0f", ax, ax, ax);
+            }
+        } else if (L->op == WO_LEAF_SPHERE && g->lit_consts) {
+            /* the centre and r^2 as VALU literal operands: o - c and r^2 - ll
+             * are single VOP2 operations (the constant needs no scalar move) */
+            bput(g->b,
+                 "%*s    float fx, fy, fz, b, ll, disc;\n"
+                 "%*s    asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fx) : \"v\"(o.x));\n"
+                 "%*s    asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fy) : \"v\"(o.y));\n"
+                 "%*s    asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fz) : \"v\"(o.z));\n"
+                 "%*s    wodev::sphere_fbl(fx, fy, fz, d, b, ll);\n"
+                 "%*s    asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(disc) : \"v\"(ll));\n"
+                 "%*s    wodev::sphere_interval_bd(b, disc, la, lb);\n",
+                 indent, "", indent, "", vl[0], indent, "", vl[1], indent, "", vl[2], indent, "", indent, "",
+                 vl[3], indent, "");
+        } else {
+            emit_consts(g->b, indent + 4, "float", nl, vl, 4);
+            bput(g->b,
+                 "%*s    wodev::%s_interval(c0, c1, c2, c3, o, d, la, lb);\n",
+                 indent, "", L->op == WO_LEAF_SPHERE ? "sphere" : "halfspace");
+        }
+        if (m == 0)
+            bput(g->b, "%*s    wodev::ivl_first(iv, la, lb);\n", indent, "");
+        else
+            bput(g->b, "%*s    wodev::ivl_meet(iv, la, lb, %uu);\n", indent, "", m);
+        bput(g->b, "%*s  }\n", indent, "");
+    }
+    for (; open_skips > 0; --open_skips) bput(g->b, "%*s  }\n", indent, "");
+}
 
 static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
     uint32_t pc = start;
@@ -168,7 +263,6 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
             pc = r->u0;
         } else if (r->op == WO_OP_PRIM) {
             uint32_t ord = r->u1, cnt = r->u0;
-            static const char* nl[4] = {"c0", "c1", "c2", "c3"};
             static const char* nk[2] = {"ka", "kb"};
             bput(g->b, "%*s{  // primitive %u (%u leaves)\n", indent, "", ord, cnt);
             if (cnt == 1u && g->fused_sphere && g->lit_consts && g->prog[pc + 1].op == WO_LEAF_SPHERE) {
@@ -177,91 +271,7 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
                 continue;
             }
             bput(g->b, "%*s  wodev::Ivl iv; float la, lb;\n", indent, "");
-            int open_skips = 0;
-            for (uint32_t m = 0; m < cnt; ++m) {
-                const WoRec* L = &g->prog[pc + 1 + m];
-                uint32_t vl[4];
-                for (int i = 0; i < 4; ++i) vl[i] = fbits(L->f[i]);
-                if (m > 0 && g->member_skip) /* empty on every lane: the other members cannot widen it */
-                    bput(g->b, "%*s  if (__ballot(!(iv.a > iv.b)) != 0ull) {\n", indent, ""), ++open_skips;
-                bput(g->b, "%*s  {\n", indent, "");
-                const WoRec* L2 = m + 1u < cnt ? &g->prog[pc + 2 + m] : NULL;
-                if (g->axis_pairs && L->op == WO_LEAF_HALFSPACE && L->u1 != 0u && L2 && L2->op == WO_LEAF_HALFSPACE &&
-                    L2->u1 == L->u1 && (L->f[L->u1 - 1u] > 0.0f) != (L2->f[L2->u1 - 1u] > 0.0f)) {
-                    /* two faces of a slab: one entry, one exit (axis_pair_meet) */
-                    static const char* nh[2] = {"c3", "c3b"};
-                    static const char axis[3] = {'x', 'y', 'z'};
-                    const char ax = axis[L->u1 - 1u];
-                    const int pos = L->f[L->u1 - 1u] > 0.0f; /* s1 = +1 */
-                    uint32_t vh[2] = {vl[3], fbits(L2->f[3])};
-                    bput(g->b, "%*s    WO_WK_N(WO_WORK_HALFSPACE_TESTS, 2u);\n", indent, "");
-                    if (m == 0) bput(g->b, "%*s    wodev::ivl_open(iv);\n", indent, "");
-                    if (g->lit_consts) {
-                        /* dist1 = h1 - s1*oa, dist2 = h2 + s1*oa with h as a literal operand */
-                        bput(g->b,
-                             "%*s    float dist1, dist2;\n"
-                             "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist1) : \"v\"(o.%c));\n"
-                             "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist2) : \"v\"(o.%c));\n"
-                             "%*s    wodev::axis_pair_meet_d(iv, %s, dist1, dist2, d.%c, iv%c, %uu, %uu);\n%*s  }\n",
-                             indent, "", indent, "", pos ? "v_sub_f32_e32" : "v_add_f32_e32", vh[0], ax, indent, "",
-                             pos ? "v_add_f32_e32" : "v_sub_f32_e32", vh[1], ax, indent, "", pos ? "1.0f" : "-1.0f", ax,
-                             ax, m, m + 1u, indent, "");
-                    } else {
-                        emit_consts(g->b, indent + 4, "float", nh, vh, 2);
-                        bput(g->b,
-                             "%*s    wodev::axis_pair_meet(iv, %s, c3, c3b, o.%c, d.%c, iv%c, %uu, %uu);\n%*s  }\n",
-                             indent, "", pos ? "1.0f" : "-1.0f", ax, ax, ax, m, m + 1u, indent, "");
-                    }
-                    ++m;
-                    continue;
-                }
-                bput(g->b, "%*s    WO_WK(%s);\n", indent, "",
-                     L->op == WO_LEAF_SPHERE ? "WO_WORK_SPHERE_TESTS" : "WO_WORK_HALFSPACE_TESTS");
-                if (L->op == WO_LEAF_HALFSPACE && L->u1 != 0u) {
-                    /* axis-aligned: s = +-1 stays a literal (inline constant), h in an SGPR */
-                    static const char* nh[1] = {"c3"};
-                    static const char axis[3] = {'x', 'y', 'z'};
-                    char ax = axis[L->u1 - 1u];
-                    const int pos = L->f[L->u1 - 1u] > 0.0f;
-                    if (g->lit_consts) {
-                        bput(g->b,
-                             "%*s    float dist;\n"
-                             "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist) : \"v\"(o.%c));\n"
-                             "%*s    wodev::halfspace_axis_dist(%s, dist, d.%c, iv%c, la, lb);\n",
-                             indent, "", indent, "", pos ? "v_sub_f32_e32" : "v_add_f32_e32", vl[3], ax, indent, "",
-                             pos ? "1.0f" : "-1.0f", ax, ax);
-                    } else {
-                        emit_consts(g->b, indent + 4, "float", nh, &vl[3], 1);
-                        bput(g->b,
-                             "%*s    wodev::halfspace_axis_interval(%s, c3, o.%c, d.%c, iv%c, la, lb);\n",
-                             indent, "", pos ? "1.0f" : "-1.0f", ax, ax, ax);
-                    }
-                } else if (L->op == WO_LEAF_SPHERE && g->lit_consts) {
-                    /* the centre and r^2 as VALU literal operands: o - c and r^2 - ll
-                     * are single VOP2 operations (the constant needs no scalar move) */
-                    bput(g->b,
-                         "%*s    float fx, fy, fz, b, ll, disc;\n"
-                         "%*s    asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fx) : \"v\"(o.x));\n"
-                         "%*s    asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fy) : \"v\"(o.y));\n"
-                         "%*s    asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fz) : \"v\"(o.z));\n"
-                         "%*s    wodev::sphere_fbl(fx, fy, fz, d, b, ll);\n"
-                         "%*s    asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(disc) : \"v\"(ll));\n"
-                         "%*s    wodev::sphere_interval_bd(b, disc, la, lb);\n",
-                         indent, "", indent, "", vl[0], indent, "", vl[1], indent, "", vl[2], indent, "", indent, "",
-                         vl[3], indent, "");
-                } else {
-                    emit_consts(g->b, indent + 4, "float", nl, vl, 4);
-                    bput(g->b,
-                         "%*s    wodev::%s_interval(c0, c1, c2, c3, o, d, la, lb);\n",
-                         indent, "", L->op == WO_LEAF_SPHERE ? "sphere" : "halfspace");
-                }
-                if (m == 0)
-                    bput(g->b, "%*s    wodev::ivl_first(iv, la, lb);\n", indent, "");
-                else
-                    bput(g->b, "%*s    wodev::ivl_meet(iv, la, lb, %uu);\n", indent, "", m);
-                bput(g->b, "%*s  }\n", indent, "");
-            }
-            for (; open_skips > 0; --open_skips) bput(g->b, "%*s  }\n", indent, "");
+            gen_members(g, pc, cnt, indent);
             uint32_t vk[2] = {ord << 12, (ord << 12) | (1u << 11)};
             bput(g->b, "%*s  if (!(iv.a > iv.b)) {\n", indent, "");
             emit_consts(g->b, indent + 4, "uint32_t", nk, vk, 2);
@@ -344,6 +354,8 @@ typedef struct SPrim {
     uint32_t pc;               /* a primitive's program counter ... */
     uint32_t npc;              /* ... or, for a unit of several primitives (npc > 0), theirs */
     uint32_t pcs[SUNIT_MAX];
+    uint32_t negm;             /* term mode: bit k = pcs[k] is a complemented literal */
+    int term;                  /* term mode: the unit is a term (gen_term) */
 } SPrim;
 
 /* a primitive's bounding sphere: its smallest sphere member (an intersection lies
@@ -362,6 +374,8 @@ static int prim_sphere(const WoRec* prog, uint32_t pc, SPrim* out) {
     }
     out->pc = pc;
     out->npc = 0;
+    out->negm = 0;
+    out->term = 0;
     return found;
 }
 
@@ -395,7 +409,13 @@ static void sprim_bound(const SPrim* p, uint32_t n, double c[3], double* R) {
 }
 
 
+static void gen_term(Gen* g, const SPrim* q, int indent);
+
 static void gen_sprim(Gen* g, const SPrim* q, int indent) {
+    if (q->term) {
+        gen_term(g, q, indent);
+        return;
+    }
     if (!q->npc) {
         gen_collect(g, q->pc, q->pc + 1u + g->prog[q->pc].u0, indent);
         return;
@@ -523,13 +543,246 @@ static void gen_collect_spatial(Gen* g, const SPrim* bounded, uint32_t nb, int i
     free(p);
 }
 
+/* term mode: the unbounded terms, then the spatial hierarchy over the others */
+static void gen_collect_terms(Gen* g, int indent) {
+    for (uint32_t i = 0; i < g->ntunb && !g->err; ++i) gen_term(g, &g->tunb[i], indent);
+    if (!g->nsprims) return;
+    SPrim* p = (SPrim*)malloc(sizeof(SPrim) * g->nsprims);
+    if (!p) {
+        g->err = 1;
+        return;
+    }
+    memcpy(p, g->sprims, sizeof(SPrim) * g->nsprims); /* gen_spatial sorts in place: the same order each pass */
+    gen_spatial(g, p, g->nsprims, indent, 1);
+    free(p);
+}
+
 /* the collect of the whole program (either pass) */
 static void gen_collect_all(Gen* g, int indent) {
     g->nbound = 0;
-    if (g->spatial)
+    if (g->term_mode)
+        gen_collect_terms(g, indent);
+    else if (g->spatial)
         gen_collect_spatial(g, g->sprims, g->nsprims, indent);
     else
         gen_collect(g, 0, g->n, indent);
+}
+
+/* ---- term mode ----
+ * When the root is a union of TERMS -- conjunctions of one or two literals, a
+ * literal being a primitive or its complement (a DIFF of one primitive by
+ * another is a AND NOT b) -- and every primitive is in one term (csg32, csg256
+ * balanced), a term changes value only at an event of one of its literals X, and
+ * then exactly when the other literal holds at that key; it rises where X's
+ * literal becomes true.  One key changes one term, so the root flips where the
+ * count of true terms crosses 0.  The collect then keeps, per lane, only the
+ * smallest term transition after `after` and whether it rises (wo_device_common.h
+ * term_cands_of): no event list, no sweep; a ray that starts outside every term
+ * hits at its first transition, others re-collect after each transition that does
+ * not flip the root (rare: a ray inside one term meets its own exit first unless
+ * another term begins before it).  The same rule as the lane tracer's term mode
+ * (trace_kernels.hip extract_terms), bit for bit the general sweep's hit. */
+#define JT_LITS 2
+#define JT_NEG 0x80000000u
+typedef struct JTerm {
+    uint32_t n, lit[JT_LITS]; /* ordinal | JT_NEG for a complement */
+} JTerm;
+
+typedef struct JTSub {
+    int kind;       /* 0 conjunction (t), 1 union of terms [start, start + count) of the term list, 2 neither */
+    JTerm t;
+    uint32_t start, count;
+} JTSub;
+
+/* The root's terms (malloc'd, *nt of them), or NULL when the root is not a union of
+ * such conjunctions. */
+static JTerm* jit_terms(const WoRec* prog, uint32_t n_recs, uint32_t n_prims, uint32_t* nt) {
+    JTSub* st = (JTSub*)malloc(sizeof(JTSub) * (n_recs + 1u));
+    JTerm* tl = (JTerm*)malloc(sizeof(JTerm) * (n_prims + 1u));
+    uint32_t sp = 0, n = 0;
+    int ok = st && tl;
+    for (uint32_t pc = 0; pc < n_recs && ok;) {
+        const WoRec* r = &prog[pc];
+        if (r->op == WO_OP_PRIM) {
+            JTSub x;
+            memset(&x, 0, sizeof x);
+            x.t.n = 1;
+            x.t.lit[0] = r->u1;
+            st[sp++] = x;
+            pc += 1u + r->u0;
+            continue;
+        }
+        ++pc;
+        if (r->op == WO_OP_BOUND) continue;
+        if (sp < 2u) {
+            ok = 0;
+            break;
+        }
+        JTSub b = st[--sp], a = st[--sp], out;
+        memset(&out, 0, sizeof out);
+        out.kind = 2;
+        if (a.kind != 2 && b.kind != 2) {
+            if (r->op == WO_OP_UNION) {
+                /* the term list stays contiguous: a union child's terms were appended
+                 * when it formed, a conjunction's are appended now */
+                uint32_t start = a.kind == 1 ? a.start : (b.kind == 1 ? b.start : n);
+                if (a.kind == 0 && n < n_prims) tl[n++] = a.t;
+                if (b.kind == 0 && n < n_prims) tl[n++] = b.t;
+                out.kind = 1;
+                out.start = start;
+                out.count = n - start;
+            } else if (r->op == WO_OP_INTER && a.kind == 0 && b.kind == 0 && a.t.n + b.t.n <= JT_LITS) {
+                out = a;
+                for (uint32_t k = 0; k < b.t.n; ++k) out.t.lit[out.t.n++] = b.t.lit[k];
+            } else if (r->op == WO_OP_DIFF || r->op == WO_OP_RDIFF) {
+                const JTSub* keep = r->op == WO_OP_DIFF ? &a : &b; /* DIFF: a AND NOT b; RDIFF: b AND NOT a */
+                const JTSub* sub = r->op == WO_OP_DIFF ? &b : &a;
+                JTerm t = keep->t;
+                int good = keep->kind == 0;
+                if (good && sub->kind == 0) {
+                    good = sub->t.n == 1u && !(sub->t.lit[0] & JT_NEG) && t.n < JT_LITS;
+                    if (good) t.lit[t.n++] = sub->t.lit[0] | JT_NEG;
+                } else if (good && sub->kind == 1) {
+                    for (uint32_t i = 0; i < sub->count && good; ++i) {
+                        const JTerm* u = &tl[sub->start + i];
+                        good = u->n == 1u && !(u->lit[0] & JT_NEG) && t.n < JT_LITS;
+                        if (good) t.lit[t.n++] = u->lit[0] | JT_NEG;
+                    }
+                    if (good) n = sub->start; /* the subtrahend's terms were the last ones appended */
+                }
+                if (good) {
+                    out.kind = 0;
+                    out.t = t;
+                }
+            }
+        }
+        st[sp++] = out;
+    }
+    if (ok && sp == 1u && st[0].kind == 0 && n < n_prims + 1u) {
+        tl[n++] = st[0].t;
+    } else if (!(ok && sp == 1u && st[0].kind == 1)) {
+        ok = 0;
+    }
+    if (ok) { /* every primitive in exactly one term */
+        uint8_t* seen = (uint8_t*)calloc(n_prims ? n_prims : 1u, 1);
+        ok = seen != NULL;
+        uint32_t lits = 0;
+        for (uint32_t i = 0; i < n && ok; ++i)
+            for (uint32_t k = 0; k < tl[i].n && ok; ++k) {
+                const uint32_t o = tl[i].lit[k] & ~JT_NEG;
+                ok = o < n_prims && !seen[o];
+                if (ok) seen[o] = 1, ++lits;
+            }
+        ok = ok && lits == n_prims;
+        free(seen);
+    }
+    free(st);
+    if (!ok) {
+        free(tl);
+        return NULL;
+    }
+    *nt = n;
+    return tl;
+}
+
+/* The interval of the convex primitive at pc into `name` (declared by the caller). */
+static void gen_term_ivl(Gen* g, uint32_t pc, const char* name, int indent) {
+    bput(g->b, "%*s{\n%*s  wodev::Ivl iv; float la, lb;\n", indent, "", indent, "");
+    gen_members(g, pc, g->prog[pc].u0, indent);
+    bput(g->b, "%*s  %s = iv;\n%*s}\n", indent, "", name, indent, "");
+}
+
+/* One term: its transitions into (best, up), and at t_min its value into cnt (first pass). */
+static void gen_term(Gen* g, const SPrim* q, int indent) {
+    const int first = g->first_pass;
+    uint32_t pcs[2] = {q->pcs[0], q->npc > 1u ? q->pcs[1] : 0u};
+    int pos[2] = {!(q->negm & 1u), !(q->negm & 2u)};
+    if (q->npc > 1u && !pos[0] && pos[1]) { /* a positive literal first: it can skip the other */
+        const uint32_t t = pcs[0];
+        pcs[0] = pcs[1], pcs[1] = t;
+        pos[0] = 1, pos[1] = 0;
+    }
+    const uint32_t o0 = g->prog[pcs[0]].u1;
+    const char* after0 = first ? "" : " & (k0 > after)";
+    const char* after1 = first ? "" : " & (k1 > after)";
+    bput(g->b, "%*s{  // term: %sprimitive %u", indent, "", pos[0] ? "" : "NOT ", o0);
+    if (q->npc > 1u) bput(g->b, " AND %sprimitive %u", pos[1] ? "" : "NOT ", g->prog[pcs[1]].u1);
+    bput(g->b, "\n");
+    const WoRec* P = &g->prog[pcs[0]];
+    if (q->npc == 1u && pos[0] && P->u0 == 1u && g->prog[pcs[0] + 1u].op == WO_LEAF_SPHERE && g->lit_consts) {
+        /* a lone sphere: its interval is [-b - s, -b + s] exactly when disc >= 0, so
+         * its transitions are formed inside the branch that computes s */
+        const WoRec* L = &g->prog[pcs[0] + 1u];
+        uint32_t vl[4];
+        for (int i = 0; i < 4; ++i) vl[i] = fbits(L->f[i]);
+        bput(g->b,
+             "%*s  WO_WK(WO_WORK_SPHERE_TESTS);\n"
+             "%*s  float fx, fy, fz, b, ll, disc;\n"
+             "%*s  asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fx) : \"v\"(o.x));\n"
+             "%*s  asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fy) : \"v\"(o.y));\n"
+             "%*s  asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fz) : \"v\"(o.z));\n"
+             "%*s  wodev::sphere_fbl(fx, fy, fz, d, b, ll);\n"
+             "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(disc) : \"v\"(ll));\n"
+             "%*s  if (__ballot(wodev::sphere_need(b, disc)) != 0ull) {\n"
+             "%*s    asm volatile(\"\");\n"
+             "%*s    if (!(disc < 0.0f)) {\n"
+             "%*s      const float s = wodev::sqrt_pt(disc), nb = -b, la = nb - s, lb = nb + s;\n"
+             "%*s      uint32_t ka, kb;\n"
+             "%*s      asm volatile(\"s_mov_b32 %%0, 0x%08x\\n\\ts_mov_b32 %%1, 0x%08x\" : \"=s\"(ka), \"=s\"(kb));\n"
+             "%*s      const uint64_t k0 = wodev::event_key_lo(la, ka), k1 = wodev::event_key_lo(lb, kb);\n",
+             indent, "", indent, "", indent, "", vl[0], indent, "", vl[1], indent, "", vl[2], indent, "", indent, "",
+             vl[3], indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", o0 << 12,
+             (o0 << 12) | (1u << 11), indent, "");
+        if (first) bput(g->b, "%*s      cnt += ((la <= tmin) & (lb > tmin)) ? 1u : 0u;\n", indent, "");
+        bput(g->b,
+             "%*s      WO_WK(WO_WORK_EVENTS);\n"
+             "%*s      wodev::term_cand(k0, (la > tmin)%s, true, best, up);\n"
+             "%*s      wodev::term_cand(k1, (lb > tmin) & (lb < wodev::kInf)%s, false, best, up);\n"
+             "%*s    }\n%*s  }\n%*s}\n",
+             indent, "", indent, "", after0, indent, "", after1, indent, "", indent, "", indent, "");
+        return;
+    }
+    bput(g->b, "%*s  wodev::Ivl ia;\n", indent, "");
+    gen_term_ivl(g, pcs[0], "ia", indent + 2);
+    uint32_t vk[4] = {o0 << 12, (o0 << 12) | (1u << 11), 0u, 0u};
+    static const char* nk[4] = {"ka0", "kb0", "ka1", "kb1"};
+    if (q->npc == 1u) {
+        emit_consts(g->b, indent + 2, "uint32_t", nk, vk, 2);
+        bput(g->b, "%*s  const wodev::TermLit x = wodev::term_lit(ia, ka0, kb0);\n", indent, "");
+        if (first) bput(g->b, "%*s  cnt += %swodev::term_in0(x) ? 1u : 0u;\n", indent, "", pos[0] ? "" : "!");
+        bput(g->b,
+             "%*s  WO_WK(WO_WORK_EVENTS);\n"
+             "%*s  wodev::term_cand(x.kin, x.valid & (x.kin != 0ull)%s, %s, best, up);\n"
+             "%*s  wodev::term_cand(x.kout, x.valid & (x.kout != wodev::kEmptyKey)%s, %s, best, up);\n%*s}\n",
+             indent, "", indent, "", first ? "" : " & (x.kin > after)", pos[0] ? "true" : "false", indent, "",
+             first ? "" : " & (x.kout > after)", pos[0] ? "false" : "true", indent, "");
+        return;
+    }
+    const uint32_t o1 = g->prog[pcs[1]].u1;
+    vk[2] = o1 << 12;
+    vk[3] = (o1 << 12) | (1u << 11);
+    /* a positive first literal empty along every lane's ray: the term is false throughout */
+    if (pos[0])
+        bput(g->b, "%*s  if (__ballot(!(ia.a > ia.b) & (ia.b > tmin)) != 0ull) {\n", indent, "");
+    else
+        bput(g->b, "%*s  {\n", indent, "");
+    bput(g->b, "%*s    wodev::Ivl ib;\n", indent, "");
+    gen_term_ivl(g, pcs[1], "ib", indent + 4);
+    emit_consts(g->b, indent + 4, "uint32_t", nk, vk, 4);
+    bput(g->b,
+         "%*s    const wodev::TermLit x = wodev::term_lit(ia, ka0, kb0), y = wodev::term_lit(ib, ka1, kb1);\n",
+         indent, "");
+    if (first)
+        bput(g->b, "%*s    cnt += (%swodev::term_in0(x) & %swodev::term_in0(y)) ? 1u : 0u;\n", indent, "",
+             pos[0] ? "" : "!", pos[1] ? "" : "!");
+    bput(g->b,
+         "%*s    WO_WK(WO_WORK_EVENTS);\n"
+         "%*s    wodev::term_cands_of<%s, %s, %s>(x, y, after, best, up);\n"
+         "%*s    wodev::term_cands_of<%s, %s, %s>(y, x, after, best, up);\n"
+         "%*s  }\n%*s}\n",
+         indent, "", indent, "", pos[0] ? "true" : "false", pos[1] ? "true" : "false", first ? "true" : "false",
+         indent, "", pos[1] ? "true" : "false", pos[0] ? "true" : "false", first ? "true" : "false", indent, "",
+         indent, "");
 }
 
 /* ---- eval: value of the subtree [start, end) as named 0/1 temporaries ---- */
@@ -1267,8 +1520,102 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         if (v && *v) g.spatial_leaf = (uint32_t)strtoul(v, NULL, 10);
         if (g.spatial_leaf < 1u) g.spatial_leaf = 1u;
     }
-    SPrim* sprims = NULL;
-    if (g.spatial) {
+    /* term mode (default where the root allows it and the tree is shallow enough
+     * for the event-list path it replaces; WOLOLO_JIT_TERMS=0 keeps that path) */
+    uint32_t n_jterms = 0;
+    JTerm* jterms = NULL;
+    {
+        const char* v = getenv("WOLOLO_JIT_TERMS");
+        if (!(v && v[0] == '0') && g.lds_events && n_prims) jterms = jit_terms(prog, n_recs, n_prims, &n_jterms);
+    }
+    SPrim* tunb = NULL;
+    if (jterms) {
+        uint32_t* pc_of = (uint32_t*)malloc(sizeof(uint32_t) * n_prims);
+        SPrim* units = (SPrim*)calloc(n_jterms, sizeof(SPrim));
+        tunb = (SPrim*)calloc(n_jterms, sizeof(SPrim));
+        if (!pc_of || !units || !tunb) g.err = 1;
+        for (uint32_t pc = 0; pc_of && pc < n_recs;) {
+            if (prog[pc].op != WO_OP_PRIM) {
+                ++pc;
+                continue;
+            }
+            pc_of[prog[pc].u1] = pc;
+            pc += 1u + prog[pc].u0;
+        }
+        uint32_t nb = 0;
+        for (uint32_t i = 0; !g.err && i < n_jterms; ++i) {
+            SPrim u;
+            memset(&u, 0, sizeof u);
+            u.term = 1;
+            u.npc = jterms[i].n;
+            int have = 0;
+            for (uint32_t k = 0; k < jterms[i].n; ++k) {
+                const uint32_t lit = jterms[i].lit[k];
+                u.pcs[k] = pc_of[lit & ~JT_NEG];
+                if (lit & JT_NEG) {
+                    u.negm |= 1u << k;
+                    continue;
+                }
+                /* the term lies inside each positive literal: the smallest one's sphere bounds it */
+                SPrim b;
+                if (prim_sphere(prog, u.pcs[k], &b) && (!have || b.r < u.r)) {
+                    u.c[0] = b.c[0], u.c[1] = b.c[1], u.c[2] = b.c[2], u.r = b.r;
+                    have = 1;
+                }
+            }
+            u.pc = u.pcs[0];
+            if (have)
+                units[nb++] = u;
+            else
+                tunb[g.ntunb++] = u;
+        }
+        /* outsized units (radius > 16x the median: a ground sphere) stay out of the
+         * hierarchy, as in the primitive form below */
+        if (nb > 2u) {
+            double* rs = (double*)malloc(sizeof(double) * nb);
+            if (rs) {
+                for (uint32_t i = 0; i < nb; ++i) rs[i] = units[i].r;
+                for (uint32_t i = 1; i < nb; ++i)
+                    for (uint32_t j = i; j > 0 && rs[j - 1] > rs[j]; --j) {
+                        const double t = rs[j];
+                        rs[j] = rs[j - 1];
+                        rs[j - 1] = t;
+                    }
+                const double med = rs[nb / 2u];
+                free(rs);
+                uint32_t k = 0;
+                for (uint32_t i = 0; i < nb; ++i) {
+                    if (units[i].r > 16.0 * med)
+                        tunb[g.ntunb++] = units[i];
+                    else
+                        units[k++] = units[i];
+                }
+                nb = k;
+            } else {
+                g.err = 1;
+            }
+        }
+        free(pc_of);
+        g.term_mode = 1;
+        g.spatial = 1;
+        g.sprims = units;
+        g.nsprims = nb;
+        g.tunb = tunb;
+    }
+    SPrim* sprims = g.term_mode ? g.sprims : NULL;
+    if (g.term_mode) {
+        /* the groups it tests: a dry run of the emitter into a scratch buffer */
+        Buf scratch = {0};
+        Buf* keep = g.b;
+        g.b = &scratch;
+        g.nbound = 0;
+        g.first_pass = 1;
+        gen_collect_terms(&g, 0);
+        nbounds += g.nbound;
+        g.b = keep;
+        free(scratch.s);
+    }
+    if (g.spatial && !g.term_mode) {
         sprims = (SPrim*)malloc(sizeof(SPrim) * (n_prims ? n_prims : 1u));
         if (!sprims) g.err = 1;
         for (uint32_t pc = 0; sprims && pc < n_recs;) {
@@ -1377,7 +1724,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             free(scratch.s);
         }
     }
-    for (uint32_t i = 0; i < n_recs; ++i) nbounds += prog[i].op == WO_OP_BOUND && bound_tested(&g, i);
+    for (uint32_t i = 0; i < n_recs && !g.term_mode; ++i) nbounds += prog[i].op == WO_OP_BOUND && bound_tested(&g, i);
 
     bput(&b, "// generated by scene_jit.c: %u records, %u primitives, %u bounds\n", n_recs, n_prims, nbounds);
     /* Small programs are copied to LDS per workgroup with the materials they use:
@@ -1396,7 +1743,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     /* the incremental union count's term table, per primitive: its term's mask test */
     uint32_t n_uterms = 0, eval_ops = 0;
     UTerm* uterms = NULL;
-    if (g.union_count && n_prims) {
+    if (g.union_count && n_prims && !g.term_mode) {
         uterms = (UTerm*)malloc(sizeof(UTerm) * n_prims);
         if (!uterms) g.err = 1;
         else n_uterms = union_terms(prog, n_recs, n_prims, uterms, n_prims);
@@ -1410,12 +1757,13 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     /* the register window for deep trees holds 5 events (csg256 chain 29.5 ms at 4,
      * 27.6 at 6, 27.5 at 8; with decision lists 19.36 at 4, 18.47 at 5, 18.65 at 6) */
     if (!g.lds_events) bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW 5\n#endif\n");
+    if (g.term_mode) bput(&b, "// term mode: %u terms (%u outside the spatial hierarchy)\n", n_jterms, g.ntunb);
     /* small scenes run 8 waves per SIMD: a 7-entry LDS list keeps 8 workgroups'
      * LDS within the CU (csg32 5.24 -> 5.19 ms; csg256 balanced keeps 8 entries:
      * 15.12 vs 15.33 ms at 7) */
     if (g.lds_events && n_prims <= 64u) bput(&b, "#ifndef WO_LDS_EVENTS\n#define WO_LDS_EVENTS 7\n#endif\n");
     bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
-         g.lds_events, tree_depth(prog, n_recs), lds_prog);
+         g.lds_events && !g.term_mode, tree_depth(prog, n_recs), lds_prog);
     if (n_uterms) {
         bput(&b, "struct __attribute__((aligned(16))) WoUTerm { uint64_t m, q; uint32_t w, neg, pad0, pad1; };\n");
         bput(&b, "// root = union of %u literal-set terms: a term is true iff ((window(w) & m) == q) != neg,\n"
@@ -1475,9 +1823,50 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             if (prog[i].op == WO_LEAF_HALFSPACE && prog[i].u1 >= 1u && prog[i].u1 <= 3u) axes |= 1u << (prog[i].u1 - 1u);
         for (int a = 0; a < 3; ++a)
             if (axes & (1u << a)) bput(&b, "    const float iv%c = wodev::rcp_dir(d.%c);\n", "xyz"[a], "xyz"[a]);
+        uint32_t ncw = nbounds ? (nbounds + 31u) / 32u : 1u;
+        if (g.term_mode) {
+            bput(&b, "    uint32_t cull[%u];  // bit k: group k culled for this wave\n", ncw);
+            for (uint32_t w = 0; w < ncw; ++w) bput(&b, "    cull[%u] = 0u;\n", w);
+            bput(&b,
+                 "    // the smallest term transition after `after`, whether it rises, and the\n"
+                 "    // number of terms true at t_min\n"
+                 "    uint64_t best = wodev::kEmptyKey, after = 0ull;\n"
+                 "    bool up = false;\n"
+                 "    uint32_t cnt = 0u;\n"
+                 "    (void)after;\n"
+                 "    WO_MARK(\"collect_begin\");\n"
+                 "    {\n");
+            g.first_pass = 1;
+            gen_collect_all(&g, 6);
+            bput(&b,
+                 "    }\n"
+                 "    WO_MARK(\"collect_end\");\n"
+                 "    WO_TMARK();\n"
+                 "    if (best == wodev::kEmptyKey) return false;\n"
+                 "    const bool root = cnt != 0u;\n"
+                 "    for (;;) {\n"
+                 "      WO_WK(WO_WORK_SWEEP_STEPS);\n"
+                 "      WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);\n"
+                 "      cnt = up ? cnt + 1u : cnt - 1u;\n"
+                 "      if ((cnt != 0u) != root) { wodev::hit_from_key(best, cnt != 0u ? 1u : 0u, hit); return true; }\n"
+                 "      // the count moved without flipping the root: the next transition\n"
+                 "      after = best;\n"
+                 "      best = wodev::kEmptyKey;\n"
+                 "      WO_WK(WO_WORK_RECOLLECTS);\n"
+                 "      {\n");
+            g.first_pass = 0;
+            gen_collect_all(&g, 8);
+            bput(&b,
+                 "      }\n"
+                 "      if (best == wodev::kEmptyKey) return false;\n"
+                 "    }\n"
+                 "  }\n"
+                 "};\n");
+            eval_ops = 4;
+            goto kernel_tail;
+        }
         bput(&b, "    uint32_t bits[%u];\n", nw);
         for (uint32_t w = 0; w < nw; ++w) bput(&b, "    bits[%u] = 0u;\n", w);
-        uint32_t ncw = nbounds ? (nbounds + 31u) / 32u : 1u;
         bput(&b, "    uint32_t cull[%u];  // bit k: BOUND k culled for this wave\n", ncw);
         for (uint32_t w = 0; w < ncw; ++w) bput(&b, "    cull[%u] = 0u;\n", w);
         /* First pass (culls, membership at t_min, every event), then the sweep;
@@ -1584,6 +1973,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  "};\n");
         }
     }
+kernel_tail:
     /* Waves per SIMD the register budget is sized for (measured, 1920x1080x64):
      * csg256 balanced / chain (128 primitives) 23.7 / 38.0 ms at 6, 21.3 / 33.8 at
      * 8; csg32 (18) 5.24 ms at 7 (8 LDS events), 5.19 at 8 (7 LDS events: 8
@@ -1638,6 +2028,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     free(g.dls);
     free(uterms);
     free(sprims);
+    free(tunb);
+    free(jterms);
     if (g.err || b.oom) {
         free(b.s);
         return NULL;

@@ -23,6 +23,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -779,7 +780,8 @@ __global__ __launch_bounds__(kBlock, (kMode == 2 || kMode == 4 || kMode == 6) ? 
     if constexpr (kMode >= 2) {
         // the top levels of the BVH next to the stacks; pathtrace_block's first
         // barrier orders the copy before any walk
-        const uint32_t stack_words = (kMode >= 4 ? (bvh.depth * kBlock + 1u) / 2u : bvh.depth * kBlock);
+        constexpr bool kStack16 = LaneTracer<kMode, kCount>::kStack16;
+        const uint32_t stack_words = kStack16 ? (bvh.depth * kBlock + 1u) / 2u : bvh.depth * kBlock;
         float4* top = reinterpret_cast<float4*>(smem + ((stack_words + 3u) & ~3u));
         for (uint32_t i = threadIdx.x; i < 4u * bvh.ntop; i += kBlock) top[i] = bvh.nodes[i];
         tr.ltop = (typename LaneTracer<kMode, kCount>::LdsNodes)top;
@@ -1925,11 +1927,15 @@ static std::string jit_key(const char* src, const std::string& arch, bool count 
     // the toolchain: hiprtc's major.minor and the HIP runtime's full version
     // (patch level included: a ROCm update that changes the compiler or the
     // device libraries misses instead of loading a stale object)
-    int vmaj = 0, vmin = 0, vrt = 0;
-    (void)hiprtcVersion(&vmaj, &vmin);
-    (void)hipRuntimeGetVersion(&vrt);
-    const int ver[3] = {vmaj, vmin, vrt};
-    part((const char*)ver, sizeof ver);
+    // (queried once: hiprtcVersion waits while another thread's compile holds
+    // hiprtc's lock, which stalled draw_frame behind a background compile)
+    static const std::array<int, 3> ver = []() {
+        int vmaj = 0, vmin = 0, vrt = 0;
+        (void)hiprtcVersion(&vmaj, &vmin);
+        (void)hipRuntimeGetVersion(&vrt);
+        return std::array<int, 3>{vmaj, vmin, vrt};
+    }();
+    part((const char*)ver.data(), sizeof(int) * ver.size());
     part(arch.data(), arch.size());
     for (const std::string& o : jit_options(arch, count)) part(o.data(), o.size());
     part(kEmbed_wo_device_common_h, strlen(kEmbed_wo_device_common_h));

@@ -11,8 +11,10 @@ from csgrenderer_amd import wololo as wl
 
 
 def test_csg32_source_compiles_for_gfx950(hostonly, monkeypatch):
-    # the scene compiler's BOUND records as the culling structure (WOLOLO_JIT_SPATIAL=0);
-    # the default spatial groups are checked at the end
+    # the event-list form (WOLOLO_JIT_TERMS=0) with the scene compiler's BOUND records as
+    # the culling structure (WOLOLO_JIT_SPATIAL=0); the spatial groups and the default
+    # term form are checked at the end
+    monkeypatch.setenv("WOLOLO_JIT_TERMS", "0")
     monkeypatch.setenv("WOLOLO_JIT_SPATIAL", "0")
     r = wl.Renderer("jit", max_nodes=4096)
     scenes.build("csg32", r)
@@ -57,6 +59,23 @@ def test_csg32_source_compiles_for_gfx950(hostonly, monkeypatch):
     ngroups = len(re.findall(r"// group \d+ \((\d+) primitives\)", src))  # the first pass tests them
     assert ngroups >= 2 and "// BOUND" not in src
     assert len(re.findall(r"if \(__ballot\(!miss\) == 0ull\)", src)) == ngroups
+    nsingle = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|sphere_need|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
+    npair = len(re.findall(r"wodev::axis_pair_meet(_d)?\(", src))
+    assert nsingle + 2 * npair == 2 * nleaf
+    assert wl.jit_compile_check(src, "gfx950") == ""
+    r.close()
+    # default: the term form (the root is a union of <= 2-literal conjunctions): every leaf
+    # still intersected once per pass, each term once per pass, no event list, no sweep
+    monkeypatch.delenv("WOLOLO_JIT_TERMS")
+    r = wl.Renderer("jit", max_nodes=4096)
+    scenes.build("csg32", r)
+    src = r.jit_source()
+    m = re.search(r"// term mode: (\d+) terms", src)
+    assert m, "csg32 takes the term form"
+    nterms = int(m.group(1))
+    assert nterms == 14  # 9 pairs (3 unions of two, 3 differences, 3 lenses) + crater + rounded cube ... as terms
+    assert len(re.findall(r"\{  // term: ", src)) == 2 * nterms
+    assert "wodev::LdsWindow win" not in src and "WO_EVAL_BEGIN" not in src and "#define WO_JIT_LDS_EVENTS 0" in src
     nsingle = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|sphere_need|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
     npair = len(re.findall(r"wodev::axis_pair_meet(_d)?\(", src))
     assert nsingle + 2 * npair == 2 * nleaf
@@ -333,13 +352,15 @@ def _compile_sweep(tmp_path, src, nw, ncull):
 @pytest.mark.parametrize("knobs", [{}, {"WOLOLO_JIT_DL_EVAL": "0", "WOLOLO_JIT_UNION_COUNT": "0"},
                                    {"WOLOLO_JIT_UNION_COUNT": "2"}])
 def test_generated_root_evaluation(hostonly, monkeypatch, tmp_path, case, knobs):
-    """The generated root evaluation (flattened literal sets; decision lists for
-    chains, WOLOLO_JIT_DL_EVAL; the incremental count of a union of literal sets,
-    WOLOLO_JIT_UNION_COUNT) compiled on the host is the program's value for random
-    membership words of several densities and for every single primitive, and --
-    with the union count -- after each of a run of toggles (the sweep's events)."""
+    """The generated root evaluation of the event-list form (WOLOLO_JIT_TERMS=0;
+    flattened literal sets; decision lists for chains, WOLOLO_JIT_DL_EVAL; the
+    incremental count of a union of literal sets, WOLOLO_JIT_UNION_COUNT) compiled on
+    the host is the program's value for random membership words of several densities
+    and for every single primitive, and -- with the union count -- after each of a run
+    of toggles (the sweep's events)."""
     import ctypes
 
+    monkeypatch.setenv("WOLOLO_JIT_TERMS", "0")
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)
     r = wl.Renderer("eval", max_nodes=4096)
@@ -394,7 +415,9 @@ def test_spatial_groups_enclose_their_primitives(hostonly, monkeypatch, case):
     """Spatial collect (scene_jit.c gen_spatial): each wave-level group test's sphere
     (centre and R, R^2 as emitted) encloses the bounding sphere of every primitive the
     group skips when culled, so a culled group never hides a primitive a ray meets;
-    and every primitive is collected exactly once per pass."""
+    and every primitive is collected exactly once per pass.  (The event-list form:
+    WOLOLO_JIT_TERMS=0; the term form's groups: test_spatial_groups_enclose_their_terms.)"""
+    monkeypatch.setenv("WOLOLO_JIT_TERMS", "0")
     monkeypatch.setenv("WOLOLO_JIT_SPATIAL", "1")
     r = wl.Renderer("sp", max_nodes=4096)
     _build_case(r, case)
@@ -440,3 +463,225 @@ def test_spatial_groups_enclose_their_primitives(hostonly, monkeypatch, case):
     # every primitive once in the first pass and once in the re-collect pass
     ords_all = [int(x) for x in re.findall(r"// primitive (\d+) ", src)]
     assert sorted(ords_all) == sorted(list(range(nprim)) * 2)
+
+
+@pytest.mark.parametrize("case", ["csg32", "csg256_balanced", "unionpairs"])
+def test_spatial_groups_enclose_their_terms(hostonly, case):
+    """The term form groups terms, each bounded by its smallest positive literal's
+    smallest sphere member (a term lies inside each positive literal): every group
+    test's sphere encloses those of the terms it skips when culled, and every
+    primitive is in exactly one term, once per pass."""
+    r = wl.Renderer("sp", max_nodes=4096)
+    _build_case(r, case)
+    prog, nrec, nprim = r.program()
+    src = r.jit_source()
+    r.close()
+    assert "// term mode:" in src
+    pc_of = {prog[i].u1: i for i in range(nrec) if prog[i].op == wl.WO_OP_PRIM}
+
+    def sphere(o):
+        pc, best = pc_of[o], None
+        for m in range(prog[pc].u0):
+            L = prog[pc + 1 + m]
+            if L.op == wl.WO_LEAF_SPHERE:
+                rr = math.sqrt(L.f[3])
+                if best is None or rr < best[3]:
+                    best = (L.f[0], L.f[1], L.f[2], rr)
+        return best
+
+    term_re = re.compile(r"// term: (NOT )?primitive (\d+)(?: AND (NOT )?primitive (\d+))?")
+
+    def term_sphere(m):
+        lits = [(m.group(2), not m.group(1))] + ([(m.group(4), not m.group(3))] if m.group(4) else [])
+        cands = [sphere(int(o)) for o, pos in lits if pos]
+        cands = [c for c in cands if c]
+        return min(cands, key=lambda c: c[3]) if cands else None
+
+    lines = src.splitlines()
+    first_pass = lines[:next(i for i, l in enumerate(lines) if "WO_MARK(\"collect_end\")" in l)]
+    groups = 0
+    for i, l in enumerate(first_pass):
+        m = re.search(r"// group (\d+) \((\d+) primitives\)", l)
+        if not m:
+            continue
+        groups += 1
+        lits = re.findall(r"0x([0-9a-f]{8})", "\n".join(first_pass[i:i + 12]))
+        r2, cx, cy, cz, rad = (_f32(x) for x in lits[:5])
+        j = next(k for k in range(i, len(first_pass)) if first_pass[k].strip().startswith("if (!(cull["))
+        ind = len(first_pass[j]) - len(first_pass[j].lstrip())
+        k = j + 1
+        while not (first_pass[k].strip() == "}" and len(first_pass[k]) - len(first_pass[k].lstrip()) == ind):
+            k += 1
+        for tm in term_re.finditer("\n".join(first_pass[j:k])):
+            c = term_sphere(tm)
+            assert c is not None, "a grouped term has a bounded positive literal"
+            need = math.dist(c[:3], (cx, cy, cz)) + c[3]
+            assert need <= rad and need * need <= r2 * (1 + 1e-6), (case, m.group(1), tm.group(0), need, rad)
+    assert groups >= 1
+    ords = []
+    for tm in term_re.finditer(src):
+        ords += [int(tm.group(2))] + ([int(tm.group(4))] if tm.group(4) else [])
+    assert sorted(ords) == sorted(list(range(nprim)) * 2)
+
+
+_TERM_HARNESS = r"""
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+#include <algorithm>
+#define __device__
+#define __forceinline__ inline
+#define WO_T_MIN (1.0e-3f)
+namespace wodev {
+constexpr uint64_t kEmptyKey = ~0ull;
+constexpr float kInf = INFINITY;
+struct Ivl { float a, b; uint32_t ma, mb; };
+inline uint64_t event_key_lo(float t, uint32_t lo) {
+    uint32_t u;
+    memcpy(&u, &t, 4);
+    return ((uint64_t)u << 32) | lo;
+}
+@TERM@
+}  // namespace wodev
+using namespace wodev;
+
+static uint64_t st = 88172645463325252ull;
+static uint32_t rnd() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return (uint32_t)st; }
+static float pick(const std::vector<float>& pool) { return pool[rnd() % pool.size()]; }
+
+struct Term { int n; uint32_t ord[2]; bool pos[2]; };
+
+// the general algorithm: every primitive event in key order, the root re-evaluated
+static bool sweep(const std::vector<Ivl>& iv, const std::vector<Term>& terms, uint64_t& key, bool& after_val) {
+    const float tmin = WO_T_MIN;
+    const size_t np = iv.size();
+    std::vector<char> in(np);
+    std::vector<uint64_t> ev;
+    for (size_t p = 0; p < np; ++p) {
+        const bool ne = !(iv[p].a > iv[p].b);
+        in[p] = ne && iv[p].a <= tmin && iv[p].b > tmin;
+        if (ne && iv[p].a > tmin) ev.push_back(event_key_lo(iv[p].a, (uint32_t)p << 12));
+        if (ne && iv[p].b > tmin && iv[p].b < kInf) ev.push_back(event_key_lo(iv[p].b, ((uint32_t)p << 12) | 2048u));
+    }
+    std::sort(ev.begin(), ev.end());
+    auto root = [&]() {
+        for (const Term& t : terms) {
+            bool v = true;
+            for (int k = 0; k < t.n; ++k) v = v && (t.pos[k] ? in[t.ord[k]] != 0 : in[t.ord[k]] == 0);
+            if (v) return true;
+        }
+        return false;
+    };
+    bool r = root();
+    for (uint64_t e : ev) {
+        in[((uint32_t)e) >> 12] ^= 1;
+        const bool r2 = root();
+        if (r2 != r) { key = e; after_val = r2; return true; }
+    }
+    return false;
+}
+
+// the term method, as the specialised kernel's term mode emits it
+template <bool kFirst>
+static void term_pass(const std::vector<Ivl>& iv, const std::vector<Term>& terms, uint64_t after, uint64_t& best,
+                      bool& up, uint32_t& cnt) {
+    for (const Term& t : terms) {
+        const uint32_t o0 = t.ord[0];
+        const TermLit x = term_lit(iv[o0], o0 << 12, (o0 << 12) | 2048u);
+        if (t.n == 1) {
+            if (kFirst) cnt += (t.pos[0] ? term_in0(x) : !term_in0(x)) ? 1u : 0u;
+            term_cand(x.kin, x.valid & (x.kin != 0ull) & (kFirst | (x.kin > after)), t.pos[0], best, up);
+            term_cand(x.kout, x.valid & (x.kout != kEmptyKey) & (kFirst | (x.kout > after)), !t.pos[0], best, up);
+            continue;
+        }
+        if (t.pos[0] && !x.valid) continue;  // the wave-level skip, per lane
+        const uint32_t o1 = t.ord[1];
+        const TermLit y = term_lit(iv[o1], o1 << 12, (o1 << 12) | 2048u);
+        if (kFirst)
+            cnt += ((t.pos[0] ? term_in0(x) : !term_in0(x)) & (t.pos[1] ? term_in0(y) : !term_in0(y))) ? 1u : 0u;
+        const int c = (t.pos[0] ? 2 : 0) | (t.pos[1] ? 1 : 0);
+        switch (c) {
+        case 3: term_cands_of<true, true, kFirst>(x, y, after, best, up); term_cands_of<true, true, kFirst>(y, x, after, best, up); break;
+        case 2: term_cands_of<true, false, kFirst>(x, y, after, best, up); term_cands_of<false, true, kFirst>(y, x, after, best, up); break;
+        case 1: term_cands_of<false, true, kFirst>(x, y, after, best, up); term_cands_of<true, false, kFirst>(y, x, after, best, up); break;
+        default: term_cands_of<false, false, kFirst>(x, y, after, best, up); term_cands_of<false, false, kFirst>(y, x, after, best, up); break;
+        }
+    }
+}
+
+static bool term_method(const std::vector<Ivl>& iv, const std::vector<Term>& terms, uint64_t& key, bool& after_val) {
+    uint64_t best = kEmptyKey;
+    bool up = false;
+    uint32_t cnt = 0;
+    term_pass<true>(iv, terms, 0ull, best, up, cnt);
+    if (best == kEmptyKey) return false;
+    const bool root = cnt != 0u;
+    for (;;) {
+        cnt = up ? cnt + 1u : cnt - 1u;
+        if ((cnt != 0u) != root) { key = best; after_val = cnt != 0u; return true; }
+        const uint64_t after = best;
+        best = kEmptyKey;
+        uint32_t unused = 0;
+        term_pass<false>(iv, terms, after, best, up, unused);
+        if (best == kEmptyKey) return false;
+    }
+}
+
+extern "C" long run(int rays, int* hits) {
+    const std::vector<float> pool = {-INFINITY, -2.0f, -0.5f, 0.0f, 1.0e-3f, 0.25f, 0.5f, 0.5f, 1.0f, 1.5f, 2.0f,
+                                     2.0f, 3.0f, 4.5f, INFINITY};
+    long bad = 0;
+    *hits = 0;
+    for (int r = 0; r < rays; ++r) {
+        const int nt = 1 + (int)(rnd() % 5);
+        std::vector<Term> terms;
+        std::vector<Ivl> iv;
+        for (int i = 0; i < nt; ++i) {
+            Term t;
+            t.n = 1 + (int)(rnd() % 2);
+            for (int k = 0; k < t.n; ++k) {
+                t.ord[k] = (uint32_t)iv.size();
+                t.pos[k] = (rnd() % 4) != 0;
+                Ivl v;
+                v.a = (rnd() % 3) ? pick(pool) : pick(pool) + 0.37f * (float)(rnd() % 7);
+                v.b = (rnd() % 3) ? pick(pool) : pick(pool) + 0.29f * (float)(rnd() % 9);
+                v.ma = v.mb = 0u;
+                iv.push_back(v);
+            }
+            terms.push_back(t);
+        }
+        uint64_t k1 = 0, k2 = 0;
+        bool v1 = false, v2 = false;
+        const bool h1 = sweep(iv, terms, k1, v1), h2 = term_method(iv, terms, k2, v2);
+        *hits += h1 ? 1 : 0;
+        if (h1 != h2 || (h1 && (k1 != k2 || v1 != v2))) ++bad;
+    }
+    return bad;
+}
+"""
+
+
+def test_term_transitions_match_the_sweep(tmp_path):
+    """The term mode's transition rule (wo_device_common.h, between WO_TERM_BEGIN and
+    WO_TERM_END), compiled on the host, against the general algorithm -- every
+    primitive event in key order, the root re-evaluated -- on random unions of one- and
+    two-literal terms with random polarities and intervals: empty ones, ones holding
+    t_min, unbounded ends and tied times (the key order breaks them).  Same hit key and
+    the same root after it, on every ray."""
+    import ctypes
+    import os
+    import subprocess
+
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "csgrenderer_amd", "csrc", "wo_device_common.h")).read()
+    term = hdr[hdr.index("// WO_TERM_BEGIN"):hdr.index("// WO_TERM_END")]
+    c = tmp_path / "terms.cpp"
+    c.write_text(_TERM_HARNESS.replace("@TERM@", term))
+    so = tmp_path / "terms.so"
+    subprocess.run(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-o", str(so), str(c)], check=True)
+    lib = ctypes.CDLL(str(so))
+    lib.run.restype = ctypes.c_long
+    hits = ctypes.c_int(0)
+    bad = lib.run(200000, ctypes.byref(hits))
+    assert hits.value > 50000  # the cases hit often enough to mean something
+    assert bad == 0, f"{bad} rays differ"
