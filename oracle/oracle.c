@@ -136,6 +136,11 @@ static float dot3(const float a[3], const float b[3]) { return (a[0] * b[0] + a[
 /* The path tracer's square root: sqrtf of max(x, 2^-96) (wo_device_common.h
  * sqrt_pt; the kernels' correctly rounded sequence is exact from 2^-96 up). */
 static float sqrt_pt(float x) { return sqrtf(fmaxf(x, 0x1p-96f)); }
+/* Exported for tests/test_oracle.py: the clamp must leave IEEE sqrtf untouched on [2^-96, inf]
+ * (keep the oracle tied to IEEE behaviour, not to the kernel). */
+void oracle_sqrt_pt_array(const float* in, float* out, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) out[i] = sqrt_pt(in[i]);
+}
 
 static void normalize3(float v[3]) {
     float inv = 1.0f / sqrt_pt(dot3(v, v));

@@ -129,3 +129,29 @@ def test_sincos_turn_accuracy():
         err = max(err, abs(s.value - np.sin(a)), abs(c.value - np.cos(a)))
         assert abs(s.value * s.value + c.value * c.value - 1.0) < 1e-6
     assert err < 4e-7, err
+
+
+def test_sqrt_clamp_is_ieee_sqrt_in_range():
+    """The path tracer's sqrt is sqrtf(max(x, 2^-96)). On every input at or
+    above 2^-96 it must be IEEE sqrtf bit for bit (numpy's float32 sqrt is correctly
+    rounded); only the degenerate inputs below (tiny, zero, negative) deviate from GLSL's
+    sqrt, which would give 0 or NaN there. Pins the oracle to IEEE, not to the kernel."""
+    import ctypes
+    lib = pyoracle.load()
+    fp = ctypes.POINTER(ctypes.c_float)
+    lib.oracle_sqrt_pt_array.argtypes = [fp, fp, ctypes.c_uint32]
+    rng = np.random.default_rng(7)
+    lo = np.float32(2.0 ** -96).view(np.uint32)
+    hi = np.float32(np.inf).view(np.uint32)
+    bits = np.concatenate([rng.integers(lo, hi, 400_000, dtype=np.uint32),
+                           np.arange(lo, lo + 4096, dtype=np.uint32),
+                           np.array([np.float32(1.0).view(np.uint32), hi - 1, hi], dtype=np.uint32)])
+    x = bits.view(np.float32)
+    out = np.empty_like(x)
+    lib.oracle_sqrt_pt_array(x.ctypes.data_as(fp), out.ctypes.data_as(fp), x.size)
+    assert np.array_equal(out.view(np.uint32), np.sqrt(x).view(np.uint32))
+    # below the clamp: the documented deviation (finite, = 2^-48) instead of 0 / NaN
+    low = np.array([0.0, -0.0, -1.0, 2.0 ** -100, -np.inf], dtype=np.float32)
+    out = np.empty_like(low)
+    lib.oracle_sqrt_pt_array(low.ctypes.data_as(fp), out.ctypes.data_as(fp), low.size)
+    assert np.all(out == np.float32(2.0 ** -48))
