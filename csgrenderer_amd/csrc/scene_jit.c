@@ -102,6 +102,7 @@ typedef struct Gen {
     int spatial_sah;  /* its splits by least surface area instead of at the median */
     uint32_t spatial_leaf; /* most primitives in a leaf group of that hierarchy */
     double spatial_ct;     /* group-test cost for SAH leaf decisions (0: split down to spatial_leaf) */
+    int dist_cull;         /* term mode, first pass: skip a group whose sphere begins beyond every lane's best transition */
     struct SPrim* sprims;  /* the bounded primitives it groups */
     uint32_t nsprims;
     struct SPrim* tunb;    /* term mode: terms without a bounding sphere (tested first, ungrouped) */
@@ -441,6 +442,14 @@ static void gen_spatial(Gen* g, SPrim* p, uint32_t n, int indent, int root) {
             static const char* nr[1] = {"bc3"};
             uint32_t nprim = 0;
             for (uint32_t i = 0; i < n; ++i) nprim += p[i].npc ? p[i].npc : 1u;
+            /* term mode: in the first pass a group none of whose lanes can find a transition
+             * before its best so far is skipped as well (not marked culled: the re-collect
+             * pass looks after that best).  Every transition of a term lies inside its
+             * positive literal, inside the group's sphere, so at or after tca - R (less a
+             * slack above tca's rounding: |o - c| <= |tca| + R for a ray that meets the
+             * sphere); a group that begins beyond t_min holds no term at t_min either. */
+            const int dc = g->term_mode && g->dist_cull;
+            if (dc) bput(g->b, "%*sbool gskip%u;\n", indent, "", k);
             bput(g->b, "%*s{  // group %u (%u primitives)\n%*s  WO_WK(WO_WORK_BOUND_TESTS);\n", indent, "", k, nprim,
                  indent, "");
             emit_consts(g->b, indent + 2, "float", nr, &vr2, 1);
@@ -452,12 +461,25 @@ static void gen_spatial(Gen* g, SPrim* p, uint32_t n, int indent, int root) {
                  "%*s  wodev::bound_tca_d2(ox, oy, oz, d, tca, d2);\n"
                  "%*s  asm(\"v_add_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(tr) : \"v\"(tca));\n"
                  "%*s  const bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, bc3)) | (tr < 0.0f);\n"
-                 "%*s  if (__ballot(!miss) == 0ull) cull[%u] |= %uu;\n"
-                 "%*s}\n",
+                 "%*s  if (__ballot(!miss) == 0ull) cull[%u] |= %uu;\n",
                  indent, "", indent, "", fbits(fc[0]), indent, "", fbits(fc[1]), indent, "", fbits(fc[2]), indent, "",
-                 indent, "", fbits(fR), indent, "", indent, "", k / 32, 1u << (k % 32), indent, "");
+                 indent, "", fbits(fR), indent, "", indent, "", k / 32, 1u << (k % 32));
+            if (!dc) bput(g->b, "%*s}\n", indent, "");
+            if (dc) {
+                bput(g->b,
+                     "%*s  float lo0;\n"
+                     "%*s  asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(lo0) : \"v\"(tca));\n"
+                     "%*s  const bool far = __builtin_fmaf(-1e-5f, tr, lo0) > __uint_as_float((uint32_t)(best >> 32));\n"
+                     "%*s  gskip%u = __ballot(!miss & !far) == 0ull;\n"
+                     "%*s}\n",
+                     indent, "", indent, "", fbits(fR), indent, "", indent, "", k, indent, "");
+                bput(g->b, "%*sif (!gskip%u) {\n", indent, "", k);
+            } else {
+                bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
+            }
+        } else {
+            bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
         }
-        bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
         inner = indent + 2;
     }
     /* with a group-test cost (WOLOLO_JIT_SPATIAL_CT = c > 0), a set of up to twice the
@@ -1518,6 +1540,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         g.spatial_ct = v && *v ? strtod(v, NULL) : 0.0;
         v = getenv("WOLOLO_JIT_SPATIAL_LEAF");
         if (v && *v) g.spatial_leaf = (uint32_t)strtoul(v, NULL, 10);
+        v = getenv("WOLOLO_JIT_DIST_CULL");
+        g.dist_cull = v && *v ? v[0] != '0' : 0;
         if (g.spatial_leaf < 1u) g.spatial_leaf = 1u;
     }
     /* term mode (default where the root allows it and the tree is shallow enough

@@ -312,18 +312,27 @@ constexpr uint32_t kNodeBound = 0u, kNodeSphere = 1u, kNodeGeneric = 2u;
 // bit.  A ray that starts inside some primitive (counted on the way: boxes that
 // contain the ray's start are never pruned) takes the general walk below.
 constexpr uint32_t kLeafRef = 0x80000000u, kNoRef = 0xffffffffu;
+// 16-bit refs (lane stacks, 4-wide nodes): node index or ordinal in bits 0-14, leaf flag in bit 15
+constexpr uint32_t kNoRef16 = 0xffffu;
 // term mode (extract_terms): literals per term; a literal is ordinal | kLitNeg (complement)
 constexpr uint32_t kTermLits = 2, kLitNeg = 0x80000000u, kNoLit = 0xffffffffu;
 // The lane BVH is built with at most kLaneDepthMax internal levels on any path,
 // and the per-lane LDS stack holds as many entries as the built tree has levels:
 // a walk pushes at most one sibling per ancestor, so the stack never overflows.
 constexpr uint32_t kLaneDepthMax = 24;
+#ifndef WO_LANES_WIDE_DEFAULT
+#define WO_LANES_WIDE_DEFAULT 0
+#endif
+constexpr bool kLanesWideDefault = WO_LANES_WIDE_DEFAULT != 0;  // WOLOLO_LANES_WIDE overrides
 #ifndef WO_LANES_FUSED_SPHERE
 #define WO_LANES_FUSED_SPHERE 1
 #endif
 // dynamic LDS of the BVH walk (stacks + top nodes): with the kernel's static LDS,
 // 8 workgroups of kBlock fit in a CU's 160 KB
 constexpr size_t kLanesBvhLds = 18u * 1024u;
+
+// component c (a compile-time constant after unrolling) of a float4
+__device__ __forceinline__ float f4c(const float4& v, int c) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); }
 
 // Slab test of a ray against an expanded AABB: [near, far] of the ray's overlap
 // (conservative: the boxes carry the slack; `ri` = reciprocal direction with
@@ -342,14 +351,18 @@ __device__ __forceinline__ float box_near(float4 lo, float4 hi, F3 ri, F3 oi, fl
 // (no generic-primitive code: fewer registers); 4 / 5 = 2 / 3 with 16-bit stack
 // entries (trees of < 2^15 nodes and primitives: half the stacks' LDS, left to
 // top nodes); 6 ordered BVH over the terms of a root that is a union of small
-// conjunctions (extract_terms: the leaves and the always list hold terms).
+// conjunctions (extract_terms: the leaves and the always list hold terms);
+// 7 / 8 / 9 = 3 / 2 / 6 over a 4-wide tree (lb_collapse4: four child boxes per
+// node, half the dependent node loads of a walk), always with 16-bit stacks.
 template <int kMode, bool kCountT>
 struct LaneTracer {
     static constexpr bool kCount = kCountT;
     static constexpr bool kBvh = kMode >= 2;
-    static constexpr bool kSpheresOnly = kMode == 3 || kMode == 5;
-    static constexpr bool kStack16 = kMode == 4 || kMode == 5;
-    static constexpr bool kTerms = kMode == 6;
+    static constexpr bool kWide = kMode >= 7;
+    static constexpr bool kSpheresOnly = kMode == 3 || kMode == 5 || kMode == 7;
+    static constexpr bool kStack16 = kMode == 4 || kMode == 5 || kWide;
+    static constexpr bool kTerms = kMode == 6 || kMode == 9;
+    static constexpr uint32_t kNodeF4 = kWide ? 7u : 4u;  // float4 per node
     WorkCounts wk;
     uint64_t tmark;  // section timing (counting builds)
     const WoRec* __restrict__ prog;      // full program (generic primitives, hit leaves)
@@ -536,6 +549,57 @@ struct LaneTracer {
             if (cur & kLeafRef) {
                 leaf(cur & ~kLeafRef, in_tree);
                 cur = kNoRef;
+            } else if constexpr (kWide) {
+                // four children: lo.x, hi.x, lo.y, hi.y, lo.z, hi.z of each, then the refs
+                WO_WK_N(WO_WORK_BOUND_TESTS, 4u);
+                float4 q[7];
+                if (cur < ntop) {
+                    const LdsNodes nd = ltop + 7u * cur;
+#pragma unroll
+                    for (int k = 0; k < 7; ++k) q[k] = nd[k];
+                    asm volatile("");
+                } else {
+                    const GlobalNodes nd = (GlobalNodes)lnodes + 7u * cur;
+#pragma unroll
+                    for (int k = 0; k < 7; ++k) q[k] = nd[k];
+                }
+                const float tb = best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(best >> 32));
+                // per child a sort key: the top 16 bits of max(near, 0) (monotone as an
+                // unsigned integer; the order only steers the walk) | the child's 16-bit
+                // ref; ~0 for a miss or an empty slot
+                uint32_t kk[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float ax = __builtin_fmaf(f4c(q[0], c), ri.x, -oi.x), bx = __builtin_fmaf(f4c(q[1], c), ri.x, -oi.x);
+                    const float ay = __builtin_fmaf(f4c(q[2], c), ri.y, -oi.y), by = __builtin_fmaf(f4c(q[3], c), ri.y, -oi.y);
+                    const float az = __builtin_fmaf(f4c(q[4], c), ri.z, -oi.z), bz = __builtin_fmaf(f4c(q[5], c), ri.z, -oi.z);
+                    const float n = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                    const float f = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                    const uint32_t r16 = __float_as_uint(f4c(q[6], c));
+                    const float n0 = fmaxf(n, 0.0f);
+                    const bool h = (f >= n0) & (n <= tb) & (r16 != kNoRef16);
+                    kk[c] = h ? ((__float_as_uint(n0) & 0xffff0000u) | r16) : 0xffffffffu;
+                }
+                // nearest first: a 4-key sorting network (misses sort last)
+                auto ce = [&](int i, int j) {
+                    const uint32_t lo = kk[i] < kk[j] ? kk[i] : kk[j], hi = kk[i] < kk[j] ? kk[j] : kk[i];
+                    kk[i] = lo;
+                    kk[j] = hi;
+                };
+                ce(0, 1);
+                ce(2, 3);
+                ce(0, 2);
+                ce(1, 3);
+                ce(1, 2);
+                cur = kk[0] == 0xffffffffu ? kNoRef : (kk[0] & 0x7fffu) | ((kk[0] & 0x8000u) << 16);
+                // the farther ones on the stack, farthest deepest (sp < 3 x the tree's levels)
+#pragma unroll
+                for (int c = 3; c >= 1; --c) {
+                    if (kk[c] != 0xffffffffu) {
+                        stk16[sp * kBlock] = (uint16_t)kk[c];
+                        ++sp;
+                    }
+                }
             } else {
                 WO_WK_N(WO_WORK_BOUND_TESTS, 2u);
                 float4 a0, a1, b0, b1;
@@ -756,7 +820,7 @@ struct LaneBvh {
 #define WO_LANES_BVH_MIN_WAVES 7  // rtiow_cover: 16.86 ms at 8, 16.63 at 7, 17.26 at 6
 #endif
 template <int kMode, bool kCount>
-__global__ __launch_bounds__(kBlock, (kMode == 2 || kMode == 4 || kMode == 6) ? WO_LANES_BVH_MIN_WAVES : WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
+__global__ __launch_bounds__(kBlock, (kMode == 2 || kMode == 4 || kMode == 6 || kMode >= 7) ? WO_LANES_BVH_MIN_WAVES : WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
     const WoRec* __restrict__ prog, const float4* __restrict__ gnodes, const uint32_t* __restrict__ ordpc,
     const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t ntrav, uint32_t local_rows, float4* __restrict__ out,
     unsigned long long* __restrict__ seg_slots, PathLaunch tg, LaneBvh bvh) {
@@ -783,7 +847,8 @@ __global__ __launch_bounds__(kBlock, (kMode == 2 || kMode == 4 || kMode == 6) ? 
         constexpr bool kStack16 = LaneTracer<kMode, kCount>::kStack16;
         const uint32_t stack_words = kStack16 ? (bvh.depth * kBlock + 1u) / 2u : bvh.depth * kBlock;
         float4* top = reinterpret_cast<float4*>(smem + ((stack_words + 3u) & ~3u));
-        for (uint32_t i = threadIdx.x; i < 4u * bvh.ntop; i += kBlock) top[i] = bvh.nodes[i];
+        constexpr uint32_t kNodeF4 = LaneTracer<kMode, kCount>::kNodeF4;
+        for (uint32_t i = threadIdx.x; i < kNodeF4 * bvh.ntop; i += kBlock) top[i] = bvh.nodes[i];
         tr.ltop = (typename LaneTracer<kMode, kCount>::LdsNodes)top;
         tr.ntop = bvh.ntop;
     }
@@ -1068,7 +1133,8 @@ struct WoDev {
     size_t lbvh_cap;
     uint32_t lb_nodes, lb_always, lb_root, lb_nprims;
     bool lb_spheres_only;  // every primitive is a single sphere (kMode 3 / 5)
-    bool lb_stack16;       // nodes and primitives < 2^15: 16-bit stack entries (kMode 4 / 5)
+    bool lb_stack16;       // nodes and primitives < 2^15: 16-bit stack entries (kMode 4 / 5, 7 / 8 / 9)
+    bool lb_wide;          // 4-wide nodes of 7 float4 (lb_collapse4; kMode 7 / 8 / 9)
     uint32_t lb_terms;     // term mode (kMode 6): terms the BVH's leaves and always list refer to
     uint32_t lb_term_off;  // their literals (uint2 each) at this u32 offset of d_lbvh
     uint32_t lb_top;       // nodes staged in LDS per workgroup
@@ -1472,6 +1538,101 @@ static uint32_t lb_build(std::vector<LbPrim>& prims, uint32_t b, uint32_t e, uin
     return n;
 }
 
+// 4-wide tree from lb_build's binary one (refs before the breadth-first order):
+// a node takes its two children and, while it has fewer than four, replaces the
+// internal child of largest surface area by that child's two children.  Node n
+// is written to n4[7n..7n+6]: lo.x, hi.x, lo.y, hi.y, lo.z, hi.z of the four
+// children (the binary nodes' expanded, outward-rounded boxes), then their refs
+// (kNoRef for an empty slot; lb_bfs4 turns them into 16-bit refs, kNoRef16).
+// `levels` = internal levels on the longest path.
+struct Lb4Child {
+    float lo[3], hi[3];
+    uint32_t ref;
+    double area() const {
+        const double x = (double)hi[0] - lo[0], y = (double)hi[1] - lo[1], z = (double)hi[2] - lo[2];
+        return 2.0 * (x * y + y * z + z * x);
+    }
+};
+static void lb_children2(const std::vector<float4>& n2, uint32_t n, Lb4Child out[2]) {
+    const float4* q = &n2[4u * n];
+    const float4 lo[2] = {q[0], q[2]}, hi[2] = {q[1], q[3]};
+    for (int c = 0; c < 2; ++c) {
+        out[c].lo[0] = lo[c].x, out[c].lo[1] = lo[c].y, out[c].lo[2] = lo[c].z;
+        out[c].hi[0] = hi[c].x, out[c].hi[1] = hi[c].y, out[c].hi[2] = hi[c].z;
+        memcpy(&out[c].ref, c == 0 ? &q[0].w : &q[1].w, sizeof(uint32_t));
+    }
+}
+static uint32_t lb_collapse4(const std::vector<float4>& n2, uint32_t n, std::vector<float4>& n4, uint32_t& levels) {
+    std::vector<Lb4Child> ch(2);
+    lb_children2(n2, n, ch.data());
+    while (ch.size() < 4u) {
+        int pick = -1;
+        double best = -1.0;
+        for (int i = 0; i < (int)ch.size(); ++i)
+            if (!(ch[i].ref & kLeafRef) && ch[i].area() > best) best = ch[i].area(), pick = i;
+        if (pick < 0) break;
+        Lb4Child sub[2];
+        lb_children2(n2, ch[pick].ref, sub);
+        ch[pick] = sub[0];
+        ch.push_back(sub[1]);
+    }
+    const uint32_t me = (uint32_t)(n4.size() / 7u);
+    n4.resize(n4.size() + 7u);
+    levels = 1u;
+    uint32_t refs[4];
+    for (uint32_t i = 0; i < 4u; ++i) {
+        if (i >= ch.size()) {
+            refs[i] = kNoRef;
+        } else if (ch[i].ref & kLeafRef) {
+            refs[i] = ch[i].ref;
+        } else {
+            uint32_t lv = 0;
+            refs[i] = lb_collapse4(n2, ch[i].ref, n4, lv);
+            levels = std::max(levels, 1u + lv);
+        }
+    }
+    float v[7][4];
+    for (uint32_t i = 0; i < 4u; ++i) {
+        const bool has = i < ch.size();
+        for (int a = 0; a < 3; ++a) {
+            v[2 * a][i] = has ? ch[i].lo[a] : 0.0f;
+            v[2 * a + 1][i] = has ? ch[i].hi[a] : 0.0f;
+        }
+        memcpy(&v[6][i], &refs[i], sizeof(float));  // full refs here; 16-bit after lb_bfs4
+    }
+    for (int k = 0; k < 7; ++k) n4[7u * me + (uint32_t)k] = make_float4(v[k][0], v[k][1], v[k][2], v[k][3]);
+    return me;
+}
+// breadth-first order of a 4-wide tree rooted at node `root` (the root becomes 0)
+static void lb_bfs4(std::vector<float4>& n4, uint32_t root) {
+    const uint32_t nn = (uint32_t)(n4.size() / 7u);
+    auto ref_at = [&](uint32_t n, int c) {
+        uint32_t u;
+        memcpy(&u, reinterpret_cast<const float*>(&n4[7u * n + 6u]) + c, sizeof u);
+        return u;
+    };
+    std::vector<uint32_t> order, newidx(nn, 0u);
+    order.push_back(root);
+    for (size_t h = 0; h < order.size(); ++h)
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t r = ref_at(order[h], c);
+            if (r != kNoRef && !(r & kLeafRef)) order.push_back(r);
+        }
+    for (uint32_t i = 0; i < nn; ++i) newidx[order[i]] = i;
+    std::vector<float4> bfs(n4.size());
+    for (uint32_t i = 0; i < nn; ++i) {
+        for (int k = 0; k < 7; ++k) bfs[7u * i + (uint32_t)k] = n4[7u * order[i] + (uint32_t)k];
+        for (int c = 0; c < 4; ++c) {
+            uint32_t r = ref_at(order[i], c);
+            if (r != kNoRef && !(r & kLeafRef)) r = newidx[r];
+            // 16-bit form (the kernel's sort keys and stack entries; refs < 2^15 checked by the caller)
+            r = r == kNoRef ? kNoRef16 : ((r & 0x7fffu) | ((r >> 16) & 0x8000u));
+            memcpy(reinterpret_cast<float*>(&bfs[7u * i + 6u]) + c, &r, sizeof r);
+        }
+    }
+    n4.swap(bfs);
+}
+
 // ---- union of conjunctions (the lane tracer's term mode) ----
 // A program whose root is a union of TERMS, each a conjunction of at most
 // kTermLits literals (a primitive or its complement: a DIFF of one primitive by
@@ -1577,6 +1738,7 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     dev->lb_nprims = n_prims;
     dev->lb_spheres_only = false;
     dev->lb_stack16 = false;
+    dev->lb_wide = false;
     dev->lb_terms = 0;
     const char* env = getenv("WOLOLO_LANES_BVH");
     if (env && env[0] == '0') return 0;
@@ -1697,9 +1859,25 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
         if (levels > kLaneDepthMax) levels = kLaneDepthMax;
         LbBox root_box;
         dev->lb_root = lb_build(prims, 0u, (uint32_t)prims.size(), levels, nodes, root_box, dev->lb_depth);
+        // 4-wide nodes (WOLOLO_LANES_WIDE=1): refs must fit the 16-bit stack entries
+        const char* wv = getenv("WOLOLO_LANES_WIDE");
+        const bool want_wide = wv ? wv[0] == '1' : kLanesWideDefault;
+        const uint32_t nrefs = terms.empty() ? n_prims : (uint32_t)terms.size();
+        if (want_wide && !(dev->lb_root & kLeafRef) && nrefs < 0x8000u) {
+            std::vector<float4> n4;
+            uint32_t lv4 = 0;
+            const uint32_t r4 = lb_collapse4(nodes, dev->lb_root, n4, lv4);
+            if (n4.size() / 7u < 0x8000u) {
+                lb_bfs4(n4, r4);
+                nodes.swap(n4);
+                dev->lb_root = 0u;
+                dev->lb_wide = true;
+                dev->lb_depth = 3u * lv4;  // stack entries: at most three siblings per level
+            }
+        }
         // breadth-first node order: the top levels are then nodes [0, k), the ones
         // every walk visits first, and they are staged in LDS (lb_top)
-        if (!(dev->lb_root & kLeafRef)) {
+        if (!dev->lb_wide && !(dev->lb_root & kLeafRef)) {
             const uint32_t nn = (uint32_t)(nodes.size() / 4u);
             auto ref_at = [&](uint32_t n, int c) {
                 uint32_t u;
@@ -1728,16 +1906,18 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
             dev->lb_root = 0u;
         }
     }
-    dev->lb_nodes = (uint32_t)(nodes.size() / 4u);
+    const uint32_t node_f4 = dev->lb_wide ? 7u : 4u;
+    dev->lb_nodes = (uint32_t)(nodes.size() / node_f4);
     dev->lb_always = (uint32_t)always.size();
     {
-        // 16-bit stack entries when every ref fits 15 bits (WOLOLO_LANES_STACK16=0: 32-bit)
+        // 16-bit stack entries when every ref fits 15 bits (WOLOLO_LANES_STACK16=1; always for 4-wide nodes)
         const char* s16 = getenv("WOLOLO_LANES_STACK16");
-        dev->lb_stack16 = terms.empty() && dev->lb_nodes < 0x8000u && n_prims < 0x8000u && s16 && s16[0] == '1';
+        dev->lb_stack16 = dev->lb_wide ||
+                          (terms.empty() && dev->lb_nodes < 0x8000u && n_prims < 0x8000u && s16 && s16[0] == '1');
         // the top nodes fill what the stacks leave of kLanesBvhLds (8 workgroups per CU)
         const size_t stacks =
             ((((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u)) + 15u) & ~(size_t)15u);
-        uint32_t top = stacks < kLanesBvhLds ? (uint32_t)((kLanesBvhLds - stacks) / (4u * sizeof(float4))) : 0u;
+        uint32_t top = stacks < kLanesBvhLds ? (uint32_t)((kLanesBvhLds - stacks) / (node_f4 * sizeof(float4))) : 0u;
         const char* v = getenv("WOLOLO_LANES_TOP");
         if (v && *v) top = (uint32_t)strtoul(v, NULL, 10);
         dev->lb_top = top < dev->lb_nodes ? top : dev->lb_nodes;
@@ -1769,9 +1949,10 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
 
 static LaneBvh lane_bvh(const WoDev* dev) {
     LaneBvh b;
+    const uint32_t node_f4 = dev->lb_wide ? 7u : 4u;
     b.nodes = dev->d_lbvh;
-    b.geo = dev->d_lbvh + 4u * dev->lb_nodes;
-    b.kind = reinterpret_cast<const uint32_t*>(dev->d_lbvh + 4u * dev->lb_nodes + dev->lb_nprims);
+    b.geo = dev->d_lbvh + node_f4 * dev->lb_nodes;
+    b.kind = reinterpret_cast<const uint32_t*>(dev->d_lbvh + node_f4 * dev->lb_nodes + dev->lb_nprims);
     b.nalways = dev->lb_always;
     b.root = dev->lb_root;
     b.nprims = dev->lb_nprims;
@@ -2215,8 +2396,8 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
     return wo_dev_launch_ex(dev, frame_in, d_out, stream_v, d_segments, nullptr, 0u, err, errlen);
 }
 
-enum PathKind { kLanesLds, kLanesGlobal, kLanesBvh, kLanesBvhSpheres, kLanesBvh16, kLanesBvhSpheres16, kLanesTerms, kJit,
-                kInterpLds, kInterpGlobal };
+enum PathKind { kLanesLds, kLanesGlobal, kLanesBvh, kLanesBvhSpheres, kLanesBvh16, kLanesBvhSpheres16, kLanesTerms,
+                kLanesWideSpheres, kLanesWide, kLanesWideTerms, kJit, kInterpLds, kInterpGlobal };
 
 template <bool kCount>
 static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
@@ -2235,6 +2416,12 @@ static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<5, kCount>, kBlock, dyn_lds);
     case kLanesTerms:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<6, kCount>, kBlock, dyn_lds);
+    case kLanesWideSpheres:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<7, kCount>, kBlock, dyn_lds);
+    case kLanesWide:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<8, kCount>, kBlock, dyn_lds);
+    case kLanesWideTerms:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<9, kCount>, kBlock, dyn_lds);
     case kInterpLds:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_kernel<true, kCount>, kBlock, dyn_lds);
     default:
@@ -2279,6 +2466,21 @@ static void static_launch(PathKind kind, dim3 grid, size_t dyn_lds, hipStream_t 
         break;
     case kLanesTerms:
         hipLaunchKernelGGL((pathtrace_lanes_kernel<6, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesWideSpheres:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<7, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesWide:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<8, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesWideTerms:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<9, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
                            dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
                            lane_bvh(dev));
         break;
@@ -2360,11 +2562,14 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
             // in LDS when it fits
             const size_t table = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
             if (dev->lb_root != kNoRef || dev->lb_always != 0u) {
-                kind = dev->lb_terms   ? kLanesTerms
-                       : dev->lb_stack16 ? (dev->lb_spheres_only ? kLanesBvhSpheres16 : kLanesBvh16)
-                                         : (dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh);
+                if (dev->lb_wide)
+                    kind = dev->lb_terms ? kLanesWideTerms : (dev->lb_spheres_only ? kLanesWideSpheres : kLanesWide);
+                else
+                    kind = dev->lb_terms   ? kLanesTerms
+                           : dev->lb_stack16 ? (dev->lb_spheres_only ? kLanesBvhSpheres16 : kLanesBvh16)
+                                             : (dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh);
                 const size_t stacks = ((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u) + 15u) & ~(size_t)15u;
-                dyn_lds = stacks + (size_t)dev->lb_top * 4u * sizeof(float4);
+                dyn_lds = stacks + (size_t)dev->lb_top * (dev->lb_wide ? 7u : 4u) * sizeof(float4);
             } else {
                 kind = table <= kLanesLdsBudget ? kLanesLds : kLanesGlobal;
                 dyn_lds = kind == kLanesLds ? table : 0u;

@@ -477,6 +477,45 @@ def test_lanes_bvh_depth_bound(levels, monkeypatch):
     r.close()
 
 
+@pytest.mark.parametrize("scene", ["union90", "rtiow_cover", "csg32", "csg256_balanced", "deep600"])
+def test_lanes_wide_bvh_bitexact(scene, monkeypatch):
+    """4-wide lane BVH (WOLOLO_LANES_WIDE=1, lb_collapse4): spheres-only (rtiow), generic
+    primitives (boxes, half-spaces: the union scene) and term mode (csg32, csg256 balanced),
+    and the 600-sphere chain whose tree is as deep as the depth bound allows (its 16-bit
+    stack holds 3 entries per level); every image the oracle's bit for bit."""
+    monkeypatch.setenv("WOLOLO_LANES_WIDE", "1")
+    monkeypatch.setenv("WOLOLO_LANES_MIN_PRIMS", "64")
+    if scene == "union90":
+        r = _union_scene()
+        p = wl.render_params(80, 60, spp=4, max_depth=8, mode=wl.MODE_PATHTRACE, seed=3)
+    elif scene == "deep600":
+        r = wl.Renderer("deep", max_nodes=4096)
+        items = []
+        for i in range(600):
+            s = r.sphere(0.05 + 0.02 * (i % 3))
+            items.append(wl.arg(s, (0.1 * (1.02 ** i - 1.0) - 3.0, 0.3 * np.sin(i), -0.2 * (i % 5))))
+        while len(items) > 1:
+            nxt = [wl.arg(r.union(items[i], items[i + 1])) for i in range(0, len(items) - 1, 2)]
+            if len(items) % 2:
+                nxt.append(items[-1])
+            items = nxt
+        r.set_camera((-3.5, 0.5, 3.0), (0.0, 0.0, -1.0), (0, 1, 0), 60.0)
+        p = wl.render_params(64, 40, spp=2, max_depth=6, mode=wl.MODE_PATHTRACE, seed=7)
+    else:
+        r, info = _scene(scene, "lanes")
+        p = info.params(width=96, height=54, spp=8, seed=7)
+    r.set_tracer("lanes")
+    for mode in (wl.MODE_NORMALS, wl.MODE_PATHTRACE):
+        p.mode = mode
+        img = r.render(p)
+        assert r.trace_path() == "lanes"
+        ref, _ = _oracle_rows(r, p)
+        _cmp(img, ref, f"wide {scene} mode={mode}")
+    info = r.lanes_info()
+    assert info["depth"] % 3 == 0 and info["depth"] <= 3 * 24, info  # 3 stack entries per 4-wide level
+    r.close()
+
+
 def test_auto_tracer_choices():
     """AUTO: the RTIOW cover (union-only, 487 primitives) takes the lane tracer; csg32 and a
     128-primitive union-only scene the JIT."""
