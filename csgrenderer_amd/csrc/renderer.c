@@ -576,8 +576,11 @@ static int sync_device_ex(Wo_Renderer* r, int may_defer) {
         const char* lm = getenv("WOLOLO_LANES_MIN_PRIMS");
         if (lm && *lm) lanes_min = (uint32_t)strtoul(lm, NULL, 10);
         int lanes_ok = wo_dev_lanes_available(r->dev);
+        /* an explicit JIT request on a scene above max_prims takes the lanes too
+         * (faster than the interpreter wherever they apply) */
         int want_lanes = lanes_ok && (r->tracer == WO_TRACER_LANES ||
-                                      (r->tracer == WO_TRACER_AUTO && r->n_prims > lanes_min));
+                                      (r->tracer == WO_TRACER_AUTO && r->n_prims > lanes_min) ||
+                                      (r->tracer == WO_TRACER_JIT && r->n_prims > max_prims));
         int want_jit = !want_lanes && r->tracer != WO_TRACER_INTERPRETER && r->n_prims > 0 && r->n_prims <= max_prims;
         for (uint32_t i = 0; i < r->ndevs; ++i) wo_dev_set_lanes(r->devs[i], want_lanes);
         r->lanes_loaded = want_lanes;

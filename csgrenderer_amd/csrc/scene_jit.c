@@ -1544,13 +1544,17 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         g.dist_cull = v && *v ? v[0] != '0' : 0;
         if (g.spatial_leaf < 1u) g.spatial_leaf = 1u;
     }
-    /* term mode (default where the root allows it and the tree is shallow enough
-     * for the event-list path it replaces; WOLOLO_JIT_TERMS=0 keeps that path) */
+    /* term mode: where the root allows it, the tree is shallow enough for the
+     * event-list path it replaces, and the scene is small enough for the spatial
+     * groups over terms to cull as well as the scene compiler's cluster hierarchy
+     * (<= 64 primitives: csg32 3.59 -> 3.33 ms; csg256 balanced 9.83 -> 12.40, so off
+     * there).  WOLOLO_JIT_TERMS=0|1 forces it either way. */
     uint32_t n_jterms = 0;
     JTerm* jterms = NULL;
     {
         const char* v = getenv("WOLOLO_JIT_TERMS");
-        if (!(v && v[0] == '0') && g.lds_events && n_prims) jterms = jit_terms(prog, n_recs, n_prims, &n_jterms);
+        const int want = v && *v ? v[0] != '0' : n_prims <= 64u;
+        if (want && g.lds_events && n_prims) jterms = jit_terms(prog, n_recs, n_prims, &n_jterms);
     }
     SPrim* tunb = NULL;
     if (jterms) {

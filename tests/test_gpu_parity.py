@@ -140,7 +140,7 @@ def _check_path(r, path, scene=None):
         want = "interpreter"
     elif path == "lanes" and _lanes_eligible(r):
         want = "lanes"
-    else:  # JIT up to WOLOLO_JIT_MAX_PRIMS (256) primitives, e.g. rtiow_cover's 487 stay interpreted
+    else:  # JIT up to WOLOLO_JIT_MAX_PRIMS (256) primitives; above, the lanes where they apply (rtiow_cover's 487)
         want = "jit" if 0 < nprim <= 256 else ("lanes" if _lanes_eligible(r) else "interpreter")
     assert r.trace_path() == want, (scene, r.trace_path(), want)
 
@@ -556,6 +556,9 @@ def test_jit_event_windows(window, monkeypatch):
     {"WOLOLO_JIT_SPATIAL": "0", "WOLOLO_JIT_UNION_COUNT": "0", "WOLOLO_JIT_DL_EVAL": "0"},
     {"WOLOLO_JIT_FLAGS": "-DWO_LDS_KEEP_SMALLEST=0"},  # a full event list keeps its first keys
     {"WOLOLO_JIT_FLAGS": "-DWO_LDS_EVENTS=3"},  # ... or its 3 smallest (overflow on most nested rays)
+    {"WOLOLO_JIT_TERMS": "1"},  # term transitions on csg256 balanced too (by default <= 64 primitives)
+    {"WOLOLO_JIT_TERMS": "0"},  # the event-list form on csg32
+    {"WOLOLO_JIT_TERMS": "1", "WOLOLO_JIT_DIST_CULL": "1"},  # groups beyond every lane's best skipped
 ])
 def test_jit_culling_knobs(knobs, monkeypatch):
     """The wave-level member skip, the bound-around-a-lone-primitive rule, the

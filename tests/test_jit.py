@@ -466,11 +466,13 @@ def test_spatial_groups_enclose_their_primitives(hostonly, monkeypatch, case):
 
 
 @pytest.mark.parametrize("case", ["csg32", "csg256_balanced", "unionpairs"])
-def test_spatial_groups_enclose_their_terms(hostonly, case):
+def test_spatial_groups_enclose_their_terms(hostonly, case, monkeypatch):
     """The term form groups terms, each bounded by its smallest positive literal's
     smallest sphere member (a term lies inside each positive literal): every group
     test's sphere encloses those of the terms it skips when culled, and every
-    primitive is in exactly one term, once per pass."""
+    primitive is in exactly one term, once per pass.  (Forced: by default the term
+    form is used up to 64 primitives.)"""
+    monkeypatch.setenv("WOLOLO_JIT_TERMS", "1")
     r = wl.Renderer("sp", max_nodes=4096)
     _build_case(r, case)
     prog, nrec, nprim = r.program()
