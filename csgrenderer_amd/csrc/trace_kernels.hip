@@ -316,6 +316,9 @@ constexpr uint32_t kLeafRef = 0x80000000u, kNoRef = 0xffffffffu;
 constexpr uint32_t kNoRef16 = 0xffffu;
 // term mode (extract_terms): literals per term; a literal is ordinal | kLitNeg (complement)
 constexpr uint32_t kTermLits = 2, kLitNeg = 0x80000000u, kNoLit = 0xffffffffu;
+// term records (build_lbvh): float4 [0] = literal 0, literal 1, kinds (2 bits per
+// literal), 0; [1 + 2x], [2 + 2x] = literal x's sphere members (centre, r^2)
+constexpr uint32_t kTermRecF4 = 5, kTermLitSphere = 1, kTermLitSphere2 = 2;  // kind 0: generic (prim_ivl)
 // The lane BVH is built with at most kLaneDepthMax internal levels on any path,
 // and the per-lane LDS stack holds as many entries as the built tree has levels:
 // a walk pushes at most one sibling per ancestor, so the stack never overflows.
@@ -374,7 +377,9 @@ struct LaneTracer {
     const float4* __restrict__ lnodes;   // 4 float4 per node: childA lo|ref, childA hi|ref B, childB lo, childB hi
     const float4* __restrict__ lgeo;     // per ordinal: sphere centre, r^2 (single-sphere primitives)
     const uint32_t* __restrict__ lkind;  // per ordinal: 1 = single sphere, 0 = generic; then the always list
-    const uint2* __restrict__ lterms;    // term mode: a term's two literals (ordinal | kLitNeg, or kNoLit)
+    // term mode: per term 5 float4 -- the two literals (ordinal | kLitNeg, or kNoLit)
+    // and their inline kinds, then per literal up to two sphere members (kTermRec*)
+    const float4* __restrict__ ltrec;
     uint32_t nalways, lroot, nprims;
     uint32_t* stk;                       // LDS stack column of this lane ([entry][lane])
     uint16_t* stk16;                     // the same with 16-bit entries (kStack16): leaf bit 15
@@ -449,20 +454,35 @@ struct LaneTracer {
         // literal becomes true (X's entry for a positive literal, its exit for a
         // complement).  A primitive is in one term, so one key changes one term.
         auto visit_term = [&](uint32_t ti, uint32_t& cnt) {
-            const uint2 tl = lterms[ti];
+            // the record's header and both literals' inline spheres: independent loads
+            const float4* rec = ltrec + kTermRecF4 * ti;
+            const float4 hd = rec[0];
+            const uint2 tl = make_uint2(__float_as_uint(hd.x), __float_as_uint(hd.y));
+            const uint32_t kinds = __float_as_uint(hd.z);
             uint64_t kin[2], kout[2];
             bool valid[2], pos[2];
 #pragma unroll
             for (int x = 0; x < 2; ++x) {
                 const uint32_t lit = x == 0 ? tl.x : tl.y;
-                kin[x] = 0ull;
-                kout[x] = kEmptyKey;
                 pos[x] = !(lit & kLitNeg);
-                valid[x] = false;
-                if (x == 1 && lit == kNoLit) continue;
                 const uint32_t ord = lit & ~kLitNeg;
-                const Ivl iv = prim_ivl(ord, o, d, inv, have_inv);
-                valid[x] = !(iv.a > iv.b) & (iv.b > tmin);
+                // an inline literal (one or two sphere members; a single sphere repeats
+                // itself as member 1, which leaves the interval and its members as
+                // they are, and a missing second literal is a dummy sphere masked out
+                // below) is branch-free: lanes at different terms stay converged
+                Ivl iv;
+                if ((kinds >> (2 * x)) & 3u) {
+                    WO_WK_N(WO_WORK_SPHERE_TESTS, ((kinds >> (2 * x)) & 3u) == kTermLitSphere ? 1u : 2u);
+                    const float4 g0 = rec[1 + 2 * x], g1 = rec[2 + 2 * x];
+                    float la, lb;
+                    sphere_interval(g0.x, g0.y, g0.z, g0.w, o, d, la, lb);
+                    ivl_first(iv, la, lb);
+                    sphere_interval(g1.x, g1.y, g1.z, g1.w, o, d, la, lb);
+                    ivl_meet(iv, la, lb, 1u);
+                } else {
+                    iv = prim_ivl(ord, o, d, inv, have_inv);
+                }
+                valid[x] = !(iv.a > iv.b) & (iv.b > tmin) & !(x == 1 && lit == kNoLit);
                 kin[x] = iv.a > tmin ? event_key(iv.a, ord, 0u, iv.ma) : 0ull;
                 kout[x] = iv.b < kInf ? event_key(iv.b, ord, 1u, iv.mb) : kEmptyKey;
             }
@@ -480,16 +500,15 @@ struct LaneTracer {
                 const int y = 1 - x;
                 const bool has = valid[x] & !(x == 1 && one);
                 const uint64_t ei = kin[x], eo = kout[x];
-                if (has & (ei != 0ull) & (ei > after) & (ei < best) && (one | lit_at(y, ei))) {
-                    WO_WK(WO_WORK_EVENTS);
-                    best = ei;
-                    best_up = pos[x];
-                }
-                if (has & (eo != kEmptyKey) & (eo > after) & (eo < best) && (one | lit_at(y, eo))) {
-                    WO_WK(WO_WORK_EVENTS);
-                    best = eo;
-                    best_up = !pos[x];
-                }
+                // selects, not branches (lanes at different terms stay converged)
+                const bool ti = has & (ei != 0ull) & (ei > after) & (ei < best) & (one | lit_at(y, ei));
+                WO_WK_N(WO_WORK_EVENTS, ti ? 1u : 0u);
+                best = ti ? ei : best;
+                best_up = ti ? pos[x] : best_up;
+                const bool to = has & (eo != kEmptyKey) & (eo > after) & (eo < best) & (one | lit_at(y, eo));
+                WO_WK_N(WO_WORK_EVENTS, to ? 1u : 0u);
+                best = to ? eo : best;
+                best_up = to ? !pos[x] : best_up;
             }
         };
         auto visit = [&](uint32_t ord, uint32_t& cnt) {
@@ -544,8 +563,15 @@ struct LaneTracer {
         };
         uint32_t in_always = 0, in_tree = 0;
         for (uint32_t i = 0; i < nalways; ++i) leaf(lkind[nprims + i], in_always);
+        // a re-query (after != 0) prunes boxes that end before the last key: their
+        // events all lie at or before it (the boxes' slack covers the slab test's
+        // rounding; the margin below covers the key's own t).  The first query
+        // keeps every box that holds the ray's start (the count at t_min).
+        const float tafter = after == 0ull ? 0.0f : __uint_as_float((uint32_t)(after >> 32));
+        const float tlo = fmaxf(__builtin_fmaf(-2e-5f, tafter, tafter) - 1e-6f, 0.0f);
         uint32_t cur = lroot, sp = 0;
         while (cur != kNoRef) {
+            WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);  // lane tracer: walk trips per wave
             if (cur & kLeafRef) {
                 leaf(cur & ~kLeafRef, in_tree);
                 cur = kNoRef;
@@ -577,7 +603,7 @@ struct LaneTracer {
                     const float f = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
                     const uint32_t r16 = __float_as_uint(f4c(q[6], c));
                     const float n0 = fmaxf(n, 0.0f);
-                    const bool h = (f >= n0) & (n <= tb) & (r16 != kNoRef16);
+                    const bool h = (f >= fmaxf(n0, tlo)) & (n <= tb) & (r16 != kNoRef16);
                     kk[c] = h ? ((__float_as_uint(n0) & 0xffff0000u) | r16) : 0xffffffffu;
                 }
                 // nearest first: a 4-key sorting network (misses sort last)
@@ -615,8 +641,8 @@ struct LaneTracer {
                 const float tb = best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(best >> 32));
                 float fa, fb;
                 const float na = box_near(a0, a1, ri, oi, fa), nb = box_near(b0, b1, ri, oi, fb);
-                const bool ha = (fa >= fmaxf(na, 0.0f)) & (na <= tb);
-                const bool hb = (fb >= fmaxf(nb, 0.0f)) & (nb <= tb);
+                const bool ha = (fa >= fmaxf(na, tlo)) & (na <= tb);
+                const bool hb = (fb >= fmaxf(nb, tlo)) & (nb <= tb);
                 const uint32_t ra = __float_as_uint(a0.w), rb = __float_as_uint(a1.w);
                 if (ha & hb) {
                     const bool a_first = na <= nb;
@@ -808,7 +834,7 @@ struct LaneBvh {
     const float4* nodes;
     const float4* geo;
     const uint32_t* kind;  // per ordinal, then the always list
-    const uint2* terms;    // term mode: two literals per term (ordinal | kLitNeg, or kNoLit)
+    const float4* trec;    // term mode: kTermRecF4 float4 per term
     uint32_t nalways, root, nprims;
     uint32_t depth;        // internal levels of the tree: the lane stack's entries
     uint32_t ntop;         // nodes [0, ntop) staged in LDS after the lane stacks
@@ -833,7 +859,7 @@ __global__ __launch_bounds__(kBlock, (kMode == 2 || kMode == 4 || kMode == 6 || 
     tr.lnodes = bvh.nodes;
     tr.lgeo = bvh.geo;
     tr.lkind = bvh.kind;
-    tr.lterms = bvh.terms;
+    tr.ltrec = bvh.trec;
     tr.nalways = bvh.nalways;
     tr.lroot = bvh.root;
     tr.nprims = bvh.nprims;
@@ -1136,7 +1162,7 @@ struct WoDev {
     bool lb_stack16;       // nodes and primitives < 2^15: 16-bit stack entries (kMode 4 / 5, 7 / 8 / 9)
     bool lb_wide;          // 4-wide nodes of 7 float4 (lb_collapse4; kMode 7 / 8 / 9)
     uint32_t lb_terms;     // term mode (kMode 6): terms the BVH's leaves and always list refer to
-    uint32_t lb_term_off;  // their literals (uint2 each) at this u32 offset of d_lbvh
+    uint32_t lb_term_off;  // their records (kTermRecF4 float4 each) at this u32 offset of d_lbvh
     uint32_t lb_top;       // nodes staged in LDS per workgroup
     uint32_t lb_depth;     // internal levels of the lane BVH (<= kLaneDepthMax)
     unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
@@ -1793,11 +1819,33 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     // term mode: a term's box is the meet of its positive literals' boxes (its
     // value, and every change of it, lies inside each of them); a term with no
     // bounded positive literal goes to the always list
-    std::vector<uint2> term_lits;
+    std::vector<float4> term_recs;
+    auto bits_f = [](uint32_t u) {
+        float f;
+        memcpy(&f, &u, sizeof f);
+        return f;
+    };
     for (uint32_t ti = 0; ti < (uint32_t)terms.size(); ++ti) {
         const auto& t = terms[ti];
-        uint2 tl = make_uint2(t[0], t.size() > 1u ? t[1] : kNoLit);
-        term_lits.push_back(tl);
+        // inline geometry: a literal that is one sphere, or two sphere members
+        float4 rec[kTermRecF4];
+        for (uint32_t k = 0; k < kTermRecF4; ++k) rec[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        uint32_t kinds = 0;
+        for (uint32_t x = 0; x < (uint32_t)t.size(); ++x) {
+            const uint32_t pc = pc_of[t[x] & ~kLitNeg];
+            const uint32_t nm = prog[pc].u0;
+            bool spheres = nm >= 1u && nm <= 2u;
+            for (uint32_t m = 0; m < nm && spheres; ++m) spheres = prog[pc + 1u + m].op == WO_LEAF_SPHERE;
+            if (!spheres) continue;
+            kinds |= (nm == 1u ? kTermLitSphere : kTermLitSphere2) << (2u * x);
+            for (uint32_t m = 0; m < 2u; ++m) {  // a single sphere repeats as member 1 (a no-op meet)
+                const WoRec& L = prog[pc + 1u + (m < nm ? m : 0u)];
+                rec[1u + 2u * x + m] = make_float4(L.f[0], L.f[1], L.f[2], L.f[3]);
+            }
+        }
+        if (t.size() == 1u) kinds |= kTermLitSphere << 2u;  // no second literal: a dummy sphere, masked out
+        rec[0] = make_float4(bits_f(t[0]), bits_f(t.size() > 1u ? t[1] : kNoLit), bits_f(kinds), 0.0f);
+        term_recs.insert(term_recs.end(), rec, rec + kTermRecF4);
         LbPrim p;
         p.ord = ti;
         bool bounded = false;
@@ -1925,12 +1973,12 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     dev->lb_spheres_only = terms.empty() && std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
     dev->lb_terms = (uint32_t)terms.size();
     const size_t f4 = nodes.size() + n_prims;
-    // ... | kind per ordinal | always list | (term mode) uint2 literals per term, 8-byte aligned
+    // ... | kind per ordinal | always list | (term mode) kTermRecF4 float4 per term, 16-byte aligned
     size_t words = (size_t)n_prims + always.size();
-    words = (words + 1u) & ~(size_t)1u;
+    words = (words + 3u) & ~(size_t)3u;
     const size_t term_off = f4 * sizeof(float4) + words * sizeof(uint32_t);
     dev->lb_term_off = (uint32_t)(term_off / sizeof(uint32_t));
-    const size_t bytes = term_off + term_lits.size() * sizeof(uint2);
+    const size_t bytes = term_off + term_recs.size() * sizeof(float4);
     if (ensure_buffer(&dev->d_lbvh, &dev->lbvh_cap, bytes, err, errlen)) return -1;
     std::vector<char> blob(bytes);
     memcpy(blob.data(), nodes.data(), nodes.size() * sizeof(float4));
@@ -1938,7 +1986,7 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     memcpy(blob.data() + f4 * sizeof(float4), kind.data(), n_prims * sizeof(uint32_t));
     memcpy(blob.data() + f4 * sizeof(float4) + n_prims * sizeof(uint32_t), always.data(),
            always.size() * sizeof(uint32_t));
-    if (!term_lits.empty()) memcpy(blob.data() + term_off, term_lits.data(), term_lits.size() * sizeof(uint2));
+    if (!term_recs.empty()) memcpy(blob.data() + term_off, term_recs.data(), term_recs.size() * sizeof(float4));
     hipError_t e = hipMemcpy(dev->d_lbvh, blob.data(), bytes, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         set_err(err, errlen, "hipMemcpy(lane BVH)", e);
@@ -1958,9 +2006,9 @@ static LaneBvh lane_bvh(const WoDev* dev) {
     b.nprims = dev->lb_nprims;
     b.ntop = dev->lb_top;
     b.depth = dev->lb_depth;
-    b.terms = dev->lb_terms ? reinterpret_cast<const uint2*>(reinterpret_cast<const uint32_t*>(dev->d_lbvh) +
+    b.trec = dev->lb_terms ? reinterpret_cast<const float4*>(reinterpret_cast<const uint32_t*>(dev->d_lbvh) +
                                                             dev->lb_term_off)
-                            : nullptr;
+                           : nullptr;
     return b;
 }
 
