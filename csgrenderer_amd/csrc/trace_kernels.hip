@@ -846,7 +846,12 @@ struct LaneBvh {
 #define WO_LANES_BVH_MIN_WAVES 7  // rtiow_cover: 16.86 ms at 8, 16.63 at 7, 17.26 at 6
 #endif
 template <int kMode, bool kCount>
-__global__ __launch_bounds__(kBlock, (kMode == 2 || kMode == 4 || kMode == 6 || kMode >= 7) ? WO_LANES_BVH_MIN_WAVES : WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
+#ifndef WO_LANES_TERMS_MIN_WAVES
+#define WO_LANES_TERMS_MIN_WAVES 7  // csg512_balanced: 80.8 ms at 7 (13 VGPRs spilled), 82.0 at 6 (none)
+#endif
+__global__ __launch_bounds__(kBlock, (kMode == 6 || kMode == 9) ? WO_LANES_TERMS_MIN_WAVES
+                                    : (kMode == 2 || kMode == 4 || kMode >= 7) ? WO_LANES_BVH_MIN_WAVES
+                                                                               : WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
     const WoRec* __restrict__ prog, const float4* __restrict__ gnodes, const uint32_t* __restrict__ ordpc,
     const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t ntrav, uint32_t local_rows, float4* __restrict__ out,
     unsigned long long* __restrict__ seg_slots, PathLaunch tg, LaneBvh bvh) {
@@ -1908,8 +1913,11 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
         LbBox root_box;
         dev->lb_root = lb_build(prims, 0u, (uint32_t)prims.size(), levels, nodes, root_box, dev->lb_depth);
         // 4-wide nodes (WOLOLO_LANES_WIDE=1): refs must fit the 16-bit stack entries
+        // default: term mode over more than 256 terms (csg512_balanced 82.0 -> 70.5 ms;
+        // neutral on csg256 balanced's 65 terms, 16.4 / 16.5 ms; slower on csg32's 14,
+        // 8.9 -> 9.6, and on the RTIOW cover's spheres, 11.7 -> 13.7)
         const char* wv = getenv("WOLOLO_LANES_WIDE");
-        const bool want_wide = wv ? wv[0] == '1' : kLanesWideDefault;
+        const bool want_wide = wv && *wv ? wv[0] == '1' : (kLanesWideDefault || terms.size() > 256u);
         const uint32_t nrefs = terms.empty() ? n_prims : (uint32_t)terms.size();
         if (want_wide && !(dev->lb_root & kLeafRef) && nrefs < 0x8000u) {
             std::vector<float4> n4;
