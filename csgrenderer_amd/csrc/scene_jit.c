@@ -78,6 +78,19 @@ static void emit_consts(Buf* b, int indent, const char* type, const char* names[
     bput(b, ");\n");
 }
 
+/* The same as VGPR moves (term mode's event-key constants: they end up in the
+ * low half of a VGPR key pair anyway, and as SGPRs they pushed other scalars into
+ * lane spills read back on every trace) */
+static void emit_vconsts(Buf* b, int indent, const char* type, const char* names[], const uint32_t* vals, int n) {
+    bput(b, "%*s%s %s", indent, "", type, names[0]);
+    for (int i = 1; i < n; ++i) bput(b, ", %s", names[i]);
+    bput(b, ";\n%*sasm volatile(\"", indent, "");
+    for (int i = 0; i < n; ++i) bput(b, "%sv_mov_b32 %%%d, 0x%08x", i ? "\\n\\t" : "", i, vals[i]);
+    bput(b, "\" : ");
+    for (int i = 0; i < n; ++i) bput(b, "%s\"=v\"(%s)", i ? ", " : "", names[i]);
+    bput(b, ");\n");
+}
+
 typedef struct Gen {
     const WoRec* prog;
     uint32_t n;
@@ -103,6 +116,7 @@ typedef struct Gen {
     uint32_t spatial_leaf; /* most primitives in a leaf group of that hierarchy */
     double spatial_ct;     /* group-test cost for SAH leaf decisions (0: split down to spatial_leaf) */
     int dist_cull;         /* term mode, first pass: skip a group whose sphere begins beyond every lane's best transition */
+    int key_vmov;          /* term mode: event-key constants by v_mov (VGPRs) instead of s_mov */
     struct SPrim* sprims;  /* the bounded primitives it groups */
     uint32_t nsprims;
     struct SPrim* tunb;    /* term mode: terms without a bounding sphere (tested first, ungrouped) */
@@ -750,11 +764,12 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
              "%*s    if (!(disc < 0.0f)) {\n"
              "%*s      const float s = wodev::sqrt_pt(disc), nb = -b, la = nb - s, lb = nb + s;\n"
              "%*s      uint32_t ka, kb;\n"
-             "%*s      asm volatile(\"s_mov_b32 %%0, 0x%08x\\n\\ts_mov_b32 %%1, 0x%08x\" : \"=s\"(ka), \"=s\"(kb));\n"
+             "%*s      asm volatile(\"%s %%0, 0x%08x\\n\\t%s %%1, 0x%08x\" : \"=%s\"(ka), \"=%s\"(kb));\n"
              "%*s      const uint64_t k0 = wodev::event_key_lo(la, ka), k1 = wodev::event_key_lo(lb, kb);\n",
              indent, "", indent, "", indent, "", vl[0], indent, "", vl[1], indent, "", vl[2], indent, "", indent, "",
-             vl[3], indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", o0 << 12,
-             (o0 << 12) | (1u << 11), indent, "");
+             vl[3], indent, "", indent, "", indent, "", indent, "", indent, "", indent, "",
+             g->key_vmov ? "v_mov_b32" : "s_mov_b32", o0 << 12, g->key_vmov ? "v_mov_b32" : "s_mov_b32",
+             (o0 << 12) | (1u << 11), g->key_vmov ? "v" : "s", g->key_vmov ? "v" : "s", indent, "");
         if (first) bput(g->b, "%*s      cnt += ((la <= tmin) & (lb > tmin)) ? 1u : 0u;\n", indent, "");
         bput(g->b,
              "%*s      WO_WK(WO_WORK_EVENTS);\n"
@@ -769,7 +784,7 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
     uint32_t vk[4] = {o0 << 12, (o0 << 12) | (1u << 11), 0u, 0u};
     static const char* nk[4] = {"ka0", "kb0", "ka1", "kb1"};
     if (q->npc == 1u) {
-        emit_consts(g->b, indent + 2, "uint32_t", nk, vk, 2);
+        (g->key_vmov ? emit_vconsts : emit_consts)(g->b, indent + 2, "uint32_t", nk, vk, 2);
         bput(g->b, "%*s  const wodev::TermLit x = wodev::term_lit(ia, ka0, kb0);\n", indent, "");
         if (first) bput(g->b, "%*s  cnt += %swodev::term_in0(x) ? 1u : 0u;\n", indent, "", pos[0] ? "" : "!");
         bput(g->b,
@@ -790,7 +805,7 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
         bput(g->b, "%*s  {\n", indent, "");
     bput(g->b, "%*s    wodev::Ivl ib;\n", indent, "");
     gen_term_ivl(g, pcs[1], "ib", indent + 4);
-    emit_consts(g->b, indent + 4, "uint32_t", nk, vk, 4);
+    (g->key_vmov ? emit_vconsts : emit_consts)(g->b, indent + 4, "uint32_t", nk, vk, 4);
     bput(g->b,
          "%*s    const wodev::TermLit x = wodev::term_lit(ia, ka0, kb0), y = wodev::term_lit(ib, ka1, kb1);\n",
          indent, "");
@@ -1540,6 +1555,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         g.spatial_ct = v && *v ? strtod(v, NULL) : 0.0;
         v = getenv("WOLOLO_JIT_SPATIAL_LEAF");
         if (v && *v) g.spatial_leaf = (uint32_t)strtoul(v, NULL, 10);
+        v = getenv("WOLOLO_JIT_KEY_VMOV");
+        g.key_vmov = v && *v ? v[0] != '0' : 0;
         v = getenv("WOLOLO_JIT_DIST_CULL");
         g.dist_cull = v && *v ? v[0] != '0' : 0;
         if (g.spatial_leaf < 1u) g.spatial_leaf = 1u;
