@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--prewarm-s", type=float, default=0.3,
+                    help="untimed frames before the warmup steps until this much wall time has passed (clock ramp)")
     ap.add_argument("--scene", default="csg32",
                     choices=["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain", "csg512_balanced", "csg32_union", "csg256_balanced_union",
                              "sphere256"])
@@ -221,6 +223,27 @@ def main():
                 ev.record(cs)
                 released[b] = ev
 
+    # Clock ramp: an idle GPU starts each run at low clocks and reaches its steady
+    # clock over the first ~0.3 s of work (csg32 launches 3.84 -> 3.28 ms over the
+    # first 8 frames in a rocprofv3 trace).  Untimed frames until that much wall
+    # time has passed (at most 200), then the W warmup steps, then the K timed ones.
+    # The count is fixed from the first frame's time and agreed over the ranks (every
+    # rank must run the same number of steps: each holds a collective).
+    prewarm = 0
+    if args.prewarm_s > 0:
+        step()  # the first frame may include loading the scene's code object: not timed
+        torch.cuda.synchronize()
+        t_pw = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        frame_s = max(time.perf_counter() - t_pw, 1e-4)
+        n_pw = torch.tensor([min(200, int(args.prewarm_s / frame_s) + 1)], dtype=torch.int64,
+                            device="cpu" if gloo else dev)
+        if world > 1:
+            dist.all_reduce(n_pw, op=dist.ReduceOp.MAX)
+        prewarm = 2 + int(n_pw.item())
+        for _ in range(prewarm - 2):
+            step()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -278,7 +301,7 @@ def main():
         line = report_line(args, r, info, params, world, elapsed_s, segs_all, segs_local, k_ms, work,
                            {"parallelism": parallelism, "ranks": world, "devices": min(world, ndev),
                             "launcher": "torchrun" if world_env else "none",
-                            "frames_in_flight": args.frames_in_flight})
+                            "frames_in_flight": args.frames_in_flight, "prewarm_frames": prewarm})
         if verified is not None:
             line["verified_vs_full_render"] = verified
         print(json.dumps(line), flush=True)
@@ -410,6 +433,14 @@ def single_process(args):
         r.render_frame_device(params, frames[fno[0] & 1].data_ptr(), cs.cuda_stream)
         fno[0] += 1
 
+    step()  # the first frame may include loading the scene's code object
+    torch.cuda.synchronize()
+    t_pw = time.perf_counter()
+    prewarm = 1
+    while args.prewarm_s > 0 and prewarm < 200 and time.perf_counter() - t_pw < args.prewarm_s:  # clock ramp
+        step()
+        torch.cuda.synchronize()
+        prewarm += 1
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
