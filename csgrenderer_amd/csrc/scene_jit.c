@@ -117,6 +117,7 @@ typedef struct Gen {
     double spatial_ct;     /* group-test cost for SAH leaf decisions (0: split down to spatial_leaf) */
     int dist_cull;         /* term mode, first pass: skip a group whose sphere begins beyond every lane's best transition */
     int key_vmov;          /* term mode: event-key constants by v_mov (VGPRs) instead of s_mov */
+    int term_dist;         /* term mode: a lone sphere / a pair's second literal skipped by lanes whose best precedes it */
     struct SPrim* sprims;  /* the bounded primitives it groups */
     uint32_t nsprims;
     struct SPrim* tunb;    /* term mode: terms without a bounding sphere (tested first, ungrouped) */
@@ -751,6 +752,20 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
         const WoRec* L = &g->prog[pcs[0] + 1u];
         uint32_t vl[4];
         for (int i = 0; i < 4; ++i) vl[i] = fbits(L->f[i]);
+        /* term_dist: a lane whose best transition so far precedes the sphere's entry
+         * cannot take one of its keys, and is not inside it at t_min.  s = sqrt(disc)
+         * <= R = fl(sqrt(r^2)) (disc <= r^2; the device's sqrt is correctly rounded,
+         * and so is a float's sqrt through double), so la = fl(-b - s) >= fl(-b - R)
+         * = -fl(b + R): the lane is skipped when fl(b + R) < -t_best (no best: NaN,
+         * never skipped).  Same keys, same image. */
+        char dist[256] = "";
+        if (g->term_dist) {
+            const float R = (float)sqrt((double)L->f[3]);
+            snprintf(dist, sizeof dist,
+                     "%*s  float bR;\n%*s  asm(\"v_add_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(bR) : \"v\"(b));\n"
+                     "%*s  const bool nearer = !(bR < -__uint_as_float((uint32_t)(best >> 32)));\n",
+                     indent, "", indent, "", fbits(R), indent, "");
+        }
         bput(g->b,
              "%*s  WO_WK(WO_WORK_SPHERE_TESTS);\n"
              "%*s  float fx, fy, fz, b, ll, disc;\n"
@@ -759,7 +774,8 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
              "%*s  asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fz) : \"v\"(o.z));\n"
              "%*s  wodev::sphere_fbl(fx, fy, fz, d, b, ll);\n"
              "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(disc) : \"v\"(ll));\n"
-             "%*s  if (__ballot(wodev::sphere_need(b, disc)) != 0ull) {\n"
+             "%s"
+             "%*s  if (__ballot(wodev::sphere_need(b, disc)%s) != 0ull) {\n"
              "%*s    asm volatile(\"\");\n"
              "%*s    if (!(disc < 0.0f)) {\n"
              "%*s      const float s = wodev::sqrt_pt(disc), nb = -b, la = nb - s, lb = nb + s;\n"
@@ -767,8 +783,8 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
              "%*s      asm volatile(\"%s %%0, 0x%08x\\n\\t%s %%1, 0x%08x\" : \"=%s\"(ka), \"=%s\"(kb));\n"
              "%*s      const uint64_t k0 = wodev::event_key_lo(la, ka), k1 = wodev::event_key_lo(lb, kb);\n",
              indent, "", indent, "", indent, "", vl[0], indent, "", vl[1], indent, "", vl[2], indent, "", indent, "",
-             vl[3], indent, "", indent, "", indent, "", indent, "", indent, "", indent, "",
-             g->key_vmov ? "v_mov_b32" : "s_mov_b32", o0 << 12, g->key_vmov ? "v_mov_b32" : "s_mov_b32",
+             vl[3], dist, indent, "", g->term_dist ? " & nearer" : "", indent, "", indent, "", indent, "", indent, "",
+             indent, "", g->key_vmov ? "v_mov_b32" : "s_mov_b32", o0 << 12, g->key_vmov ? "v_mov_b32" : "s_mov_b32",
              (o0 << 12) | (1u << 11), g->key_vmov ? "v" : "s", g->key_vmov ? "v" : "s", indent, "");
         if (first) bput(g->b, "%*s      cnt += ((la <= tmin) & (lb > tmin)) ? 1u : 0u;\n", indent, "");
         bput(g->b,
@@ -799,7 +815,13 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
     vk[2] = o1 << 12;
     vk[3] = (o1 << 12) | (1u << 11);
     /* a positive first literal empty along every lane's ray: the term is false throughout */
-    if (pos[0])
+    /* term_dist: every transition of the term lies inside its positive first literal,
+     * at or after ia.a, so a lane whose best precedes ia.a skips the second literal */
+    if (pos[0] && g->term_dist)
+        bput(g->b,
+             "%*s  if (__ballot(!(ia.a > ia.b) & (ia.b > tmin) & !(ia.a > __uint_as_float((uint32_t)(best >> 32)))) != 0ull) {\n",
+             indent, "");
+    else if (pos[0])
         bput(g->b, "%*s  if (__ballot(!(ia.a > ia.b) & (ia.b > tmin)) != 0ull) {\n", indent, "");
     else
         bput(g->b, "%*s  {\n", indent, "");
@@ -1555,6 +1577,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         g.spatial_ct = v && *v ? strtod(v, NULL) : 0.0;
         v = getenv("WOLOLO_JIT_SPATIAL_LEAF");
         if (v && *v) g.spatial_leaf = (uint32_t)strtoul(v, NULL, 10);
+        v = getenv("WOLOLO_JIT_TERM_DIST");
+        g.term_dist = v && *v ? v[0] != '0' : 0;
         v = getenv("WOLOLO_JIT_KEY_VMOV");
         g.key_vmov = v && *v ? v[0] != '0' : 0;
         v = getenv("WOLOLO_JIT_DIST_CULL");

@@ -361,8 +361,9 @@ template <int kMode, bool kCountT>
 struct LaneTracer {
     static constexpr bool kCount = kCountT;
     static constexpr bool kBvh = kMode >= 2;
-    static constexpr bool kWide = kMode >= 7;
-    static constexpr bool kSpheresOnly = kMode == 3 || kMode == 5 || kMode == 7;
+    static constexpr bool kWide = kMode >= 7 && kMode <= 9;
+    static constexpr bool kGrid = kMode == 10;
+    static constexpr bool kSpheresOnly = kMode == 3 || kMode == 5 || kMode == 7 || kMode == 10;
     static constexpr bool kStack16 = kMode == 4 || kMode == 5 || kWide;
     static constexpr bool kTerms = kMode == 6 || kMode == 9;
     static constexpr uint32_t kNodeF4 = kWide ? 7u : 4u;  // float4 per node
@@ -395,6 +396,11 @@ struct LaneTracer {
 #endif
     LdsNodes ltop;
     uint32_t ntop;
+    // uniform grid (kMode 10, build_grid): cell c's ordinals are gitems[gcells[c] .. gcells[c + 1])
+    float glo[3], gh[3], ginv[3];
+    uint32_t gres[3];
+    const uint32_t* __restrict__ gcells;
+    const uint32_t* __restrict__ gitems;
 
     __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const { return prog[ordpc[h.ord] + 1u + h.member]; }
 
@@ -435,6 +441,66 @@ struct LaneTracer {
             }
         }
         return iv;
+    }
+
+    // Uniform-grid walk (3-D DDA, Amanatides & Woo): cells in ray order from the
+    // grid's entry (a re-query from the last key's t), each cell's primitives
+    // visited (a primitive spans several cells: the minimum is idempotent, and the
+    // count at t_min is taken in the first cell only, which holds every primitive
+    // containing the ray's start: build_grid bins each box grown by more than
+    // t_min).  The walk stops once the best key precedes the current cell's exit
+    // (less a margin for the DDA's rounding): every later cell, and every event in
+    // it, begins after that exit.  The cell sequence needs no loads, so the next
+    // cell's list is fetched while this one's spheres are tested.
+    template <class Visit>
+    __device__ __forceinline__ void grid_walk(F3 o, F3 d, F3 ri, F3 oi, uint64_t after, const uint64_t& best,
+                                              uint32_t& cnt, Visit& visit) {
+        const float ax0 = __builtin_fmaf(glo[0], ri.x, -oi.x), ax1 = __builtin_fmaf(glo[0] + gh[0] * (float)gres[0], ri.x, -oi.x);
+        const float ay0 = __builtin_fmaf(glo[1], ri.y, -oi.y), ay1 = __builtin_fmaf(glo[1] + gh[1] * (float)gres[1], ri.y, -oi.y);
+        const float az0 = __builtin_fmaf(glo[2], ri.z, -oi.z), az1 = __builtin_fmaf(glo[2] + gh[2] * (float)gres[2], ri.z, -oi.z);
+        const float tenter = fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1));
+        const float texit = fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1));
+        const float tafter = after == 0ull ? 0.0f : __uint_as_float((uint32_t)(after >> 32));
+        const float t0 = fmaxf(tenter, fmaxf(__builtin_fmaf(-2e-5f, tafter, tafter) - 1e-5f, 0.0f));
+        if (!(t0 <= texit)) return;
+        // the start cell (clamped: t0 may round a hair outside the grid)
+        int ix = (int)floorf(((o.x + t0 * d.x) - glo[0]) * ginv[0]);
+        int iy = (int)floorf(((o.y + t0 * d.y) - glo[1]) * ginv[1]);
+        int iz = (int)floorf(((o.z + t0 * d.z) - glo[2]) * ginv[2]);
+        ix = min(max(ix, 0), (int)gres[0] - 1);
+        iy = min(max(iy, 0), (int)gres[1] - 1);
+        iz = min(max(iz, 0), (int)gres[2] - 1);
+        // steps and per-cell t increments recomputed at use (registers: the walk runs
+        // inside the path loop at 8 waves per SIMD)
+        float tnx = __builtin_fmaf(glo[0] + gh[0] * (float)(ix + (d.x >= 0.0f)), ri.x, -oi.x);
+        float tny = __builtin_fmaf(glo[1] + gh[1] * (float)(iy + (d.y >= 0.0f)), ri.y, -oi.y);
+        float tnz = __builtin_fmaf(glo[2] + gh[2] * (float)(iz + (d.z >= 0.0f)), ri.z, -oi.z);
+        bool first = after == 0ull;
+        uint32_t unused = 0;
+        for (;;) {
+            WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);  // grid: cell trips per wave
+            WO_WK(WO_WORK_BOUND_TESTS);       // grid: cells visited
+            const uint32_t c = ((uint32_t)iz * gres[1] + (uint32_t)iy) * gres[0] + (uint32_t)ix;
+            const uint32_t b0 = gcells[c], b1 = gcells[c + 1u];
+            for (uint32_t k = b0; k < b1; ++k) visit(gitems[k], first ? cnt : unused);
+            first = false;
+            const float tc = fminf(fminf(tnx, tny), tnz);  // this cell's exit
+            const float tb = best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(best >> 32));
+            if (tb < __builtin_fmaf(-2e-5f, tc, tc) - 1e-5f) break;
+            if (tnx <= tny && tnx <= tnz) {
+                ix += d.x >= 0.0f ? 1 : -1;
+                tnx += gh[0] * fabsf(ri.x);
+                if ((uint32_t)ix >= gres[0]) break;
+            } else if (tny <= tnz) {
+                iy += d.y >= 0.0f ? 1 : -1;
+                tny += gh[1] * fabsf(ri.y);
+                if ((uint32_t)iy >= gres[1]) break;
+            } else {
+                iz += d.z >= 0.0f ? 1 : -1;
+                tnz += gh[2] * fabsf(ri.z);
+                if ((uint32_t)iz >= gres[2]) break;
+            }
+        }
     }
 
     // The smallest event key > `after` (entries and exits after t_min), or
@@ -563,6 +629,12 @@ struct LaneTracer {
         };
         uint32_t in_always = 0, in_tree = 0;
         for (uint32_t i = 0; i < nalways; ++i) leaf(lkind[nprims + i], in_always);
+        if constexpr (kGrid) {
+            grid_walk(o, d, ri, oi, after, best, in_tree, visit);
+            inside = in_always + in_tree;
+            up = !(best & kKeyTypeBit);
+            return best;
+        }
         // a re-query (after != 0) prunes boxes that end before the last key: their
         // events all lie at or before it (the boxes' slack covers the slab test's
         // rounding; the margin below covers the key's own t).  The first query
@@ -838,6 +910,10 @@ struct LaneBvh {
     uint32_t nalways, root, nprims;
     uint32_t depth;        // internal levels of the tree: the lane stack's entries
     uint32_t ntop;         // nodes [0, ntop) staged in LDS after the lane stacks
+    float glo[3], gh[3], ginv[3];  // uniform grid (kMode 10): origin, cell size, 1 / cell size
+    uint32_t gres[3];
+    const uint32_t* gcells;        // ncells + 1 offsets into gitems
+    const uint32_t* gitems;        // ordinals
 };
 
 // Dynamic LDS: the BVH walk's lane stacks ([depth][kBlock] u32) and top nodes,
@@ -850,7 +926,7 @@ template <int kMode, bool kCount>
 #define WO_LANES_TERMS_MIN_WAVES 7  // csg512_balanced: 80.8 ms at 7 (13 VGPRs spilled), 82.0 at 6 (none)
 #endif
 __global__ __launch_bounds__(kBlock, (kMode == 6 || kMode == 9) ? WO_LANES_TERMS_MIN_WAVES
-                                    : (kMode == 2 || kMode == 4 || kMode >= 7) ? WO_LANES_BVH_MIN_WAVES
+                                    : (kMode == 2 || kMode == 4 || kMode == 7 || kMode == 8) ? WO_LANES_BVH_MIN_WAVES
                                                                                : WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
     const WoRec* __restrict__ prog, const float4* __restrict__ gnodes, const uint32_t* __restrict__ ordpc,
     const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t ntrav, uint32_t local_rows, float4* __restrict__ out,
@@ -865,6 +941,15 @@ __global__ __launch_bounds__(kBlock, (kMode == 6 || kMode == 9) ? WO_LANES_TERMS
     tr.lgeo = bvh.geo;
     tr.lkind = bvh.kind;
     tr.ltrec = bvh.trec;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        tr.glo[a] = bvh.glo[a];
+        tr.gh[a] = bvh.gh[a];
+        tr.ginv[a] = bvh.ginv[a];
+        tr.gres[a] = bvh.gres[a];
+    }
+    tr.gcells = bvh.gcells;
+    tr.gitems = bvh.gitems;
     tr.nalways = bvh.nalways;
     tr.lroot = bvh.root;
     tr.nprims = bvh.nprims;
@@ -1166,6 +1251,12 @@ struct WoDev {
     bool lb_spheres_only;  // every primitive is a single sphere (kMode 3 / 5)
     bool lb_stack16;       // nodes and primitives < 2^15: 16-bit stack entries (kMode 4 / 5, 7 / 8 / 9)
     bool lb_wide;          // 4-wide nodes of 7 float4 (lb_collapse4; kMode 7 / 8 / 9)
+    bool lb_grid;          // uniform grid over single spheres (build_grid; kMode 10)
+    float g_lo[3], g_h[3];
+    uint32_t g_res[3];
+    uint32_t* d_grid;      // [ncells + 1 offsets][items]
+    size_t grid_cap;
+    uint32_t g_items_off;
     uint32_t lb_terms;     // term mode (kMode 6): terms the BVH's leaves and always list refer to
     uint32_t lb_term_off;  // their records (kTermRecF4 float4 each) at this u32 offset of d_lbvh
     uint32_t lb_top;       // nodes staged in LDS per workgroup
@@ -1287,6 +1378,7 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
     if (dev->d_frame) (void)hipFree(dev->d_frame);
     if (dev->d_trav) (void)hipFree(dev->d_trav);
     if (dev->d_lbvh) (void)hipFree(dev->d_lbvh);
+    if (dev->d_grid) (void)hipFree(dev->d_grid);
     if (dev->d_ordpc) (void)hipFree(dev->d_ordpc);
     if (dev->d_segslots) (void)hipFree(dev->d_segslots);
     if (dev->d_work) (void)hipFree(dev->d_work);
@@ -1757,6 +1849,87 @@ static bool extract_terms(WoRec const* prog, uint32_t n_recs, uint32_t n_prims,
     return true;
 }
 
+// Uniform grid over single-sphere primitives (the lane tracer's kMode 10,
+// WOLOLO_LANES_GRID=1): about `density` cells per primitive, cubic-ish cells over
+// the primitives' bounding box; each primitive is binned into every cell its box,
+// grown by kGridPad (more than t_min along a unit direction, and far more than the
+// DDA's rounding), overlaps, so the first cell holds every primitive containing the
+// ray's start and a cell the rounded walk visits instead of its true neighbour
+// still lists what the neighbour would.  Offsets (ncells + 1) then ordinals.
+static int build_grid(WoDev* dev, const std::vector<LbPrim>& prims, char* err, size_t errlen) {
+    constexpr double kGridPad = 4e-3;
+    if (prims.empty()) return 0;
+    double lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) lo[a] = INFINITY, hi[a] = -INFINITY;
+    for (const LbPrim& p : prims)
+        for (int a = 0; a < 3; ++a) lo[a] = fmin(lo[a], p.lo[a] - kGridPad), hi[a] = fmax(hi[a], p.hi[a] + kGridPad);
+    double density = 3.0;
+    if (const char* v = getenv("WOLOLO_LANES_GRID_DENSITY")) density = v[0] ? strtod(v, NULL) : density;
+    double ext[3], vol = 1.0;
+    for (int a = 0; a < 3; ++a) ext[a] = fmax(hi[a] - lo[a], 1e-6), vol *= ext[a];
+    const double h = cbrt(vol / (density * (double)prims.size()));
+    uint32_t res[3];
+    for (int a = 0; a < 3; ++a) {
+        const double r = ceil(ext[a] / h);
+        res[a] = (uint32_t)(r < 1.0 ? 1.0 : (r > 512.0 ? 512.0 : r));
+    }
+    const uint64_t ncells = (uint64_t)res[0] * res[1] * res[2];
+    if (ncells > (1u << 24)) return 0;
+    float flo[3], fh[3];
+    for (int a = 0; a < 3; ++a) {
+        flo[a] = (float)lo[a];
+        fh[a] = (float)(ext[a] / res[a]);
+    }
+    auto cell_range = [&](const LbPrim& p, int a, uint32_t& c0, uint32_t& c1) {
+        const double x0 = (p.lo[a] - kGridPad - (double)flo[a]) / (double)fh[a];
+        const double x1 = (p.hi[a] + kGridPad - (double)flo[a]) / (double)fh[a];
+        const double m = (double)res[a] - 1.0;
+        c0 = (uint32_t)fmin(fmax(floor(x0), 0.0), m);
+        c1 = (uint32_t)fmin(fmax(floor(x1), 0.0), m);
+    };
+    std::vector<uint32_t> count(ncells + 1u, 0u);
+    for (int pass = 0; pass < 2; ++pass) {
+        std::vector<uint32_t> fill;
+        if (pass == 1) {
+            for (uint64_t c = 0; c < ncells; ++c) count[c + 1u] += count[c];  // exclusive offsets
+            fill.assign(count.begin(), count.end() - 1);
+        }
+        std::vector<uint32_t> items(pass == 1 ? count[ncells] : 0u);
+        for (const LbPrim& p : prims) {
+            uint32_t r0[3], r1[3];
+            for (int a = 0; a < 3; ++a) cell_range(p, a, r0[a], r1[a]);
+            for (uint32_t z = r0[2]; z <= r1[2]; ++z)
+                for (uint32_t y = r0[1]; y <= r1[1]; ++y)
+                    for (uint32_t x = r0[0]; x <= r1[0]; ++x) {
+                        const uint64_t c = ((uint64_t)z * res[1] + y) * res[0] + x;
+                        if (pass == 0)
+                            ++count[c + 1u];
+                        else
+                            items[fill[c]++] = p.ord;
+                    }
+        }
+        if (pass == 1) {
+            const size_t bytes = (count.size() + items.size()) * sizeof(uint32_t);
+            if (ensure_buffer(&dev->d_grid, &dev->grid_cap, bytes, err, errlen)) return -1;
+            std::vector<uint32_t> blob(count);
+            blob.insert(blob.end(), items.begin(), items.end());
+            hipError_t e = hipMemcpy(dev->d_grid, blob.data(), bytes, hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                set_err(err, errlen, "hipMemcpy(lane grid)", e);
+                return -1;
+            }
+            dev->g_items_off = (uint32_t)count.size();
+        }
+    }
+    for (int a = 0; a < 3; ++a) {
+        dev->g_lo[a] = flo[a];
+        dev->g_h[a] = fh[a];
+        dev->g_res[a] = res[a];
+    }
+    dev->lb_grid = true;
+    return 0;
+}
+
 // Union-only programs: an AABB BVH over the bounded primitives (boxes expanded by
 // 1e-4 of their size and position plus 1e-5, so the approximate slab test never
 // culls a primitive the exact arithmetic meets) and the always list: unbounded
@@ -1770,6 +1943,7 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     dev->lb_spheres_only = false;
     dev->lb_stack16 = false;
     dev->lb_wide = false;
+    dev->lb_grid = false;
     dev->lb_terms = 0;
     const char* env = getenv("WOLOLO_LANES_BVH");
     if (env && env[0] == '0') return 0;
@@ -1901,6 +2075,12 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
         }
         prims.swap(kept);
     }
+    {
+        // spheres only, union only: the uniform grid on request (WOLOLO_LANES_GRID=1)
+        const char* gv = getenv("WOLOLO_LANES_GRID");
+        const bool spheres = terms.empty() && std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
+        if (spheres && gv && gv[0] == '1' && build_grid(dev, prims, err, errlen)) return -1;
+    }
     std::vector<float4> nodes;
     if (ceil_log2((uint32_t)prims.size()) > kLaneDepthMax) return 0;  // > 2^24 primitives: the general walk
     if (!prims.empty()) {
@@ -1977,6 +2157,7 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
         const char* v = getenv("WOLOLO_LANES_TOP");
         if (v && *v) top = (uint32_t)strtoul(v, NULL, 10);
         dev->lb_top = top < dev->lb_nodes ? top : dev->lb_nodes;
+        if (dev->lb_grid) dev->lb_top = 0;  // the grid walk reads no nodes
     }
     dev->lb_spheres_only = terms.empty() && std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
     dev->lb_terms = (uint32_t)terms.size();
@@ -2014,6 +2195,14 @@ static LaneBvh lane_bvh(const WoDev* dev) {
     b.nprims = dev->lb_nprims;
     b.ntop = dev->lb_top;
     b.depth = dev->lb_depth;
+    for (int a = 0; a < 3; ++a) {
+        b.glo[a] = dev->g_lo[a];
+        b.gh[a] = dev->g_h[a];
+        b.ginv[a] = dev->lb_grid ? 1.0f / dev->g_h[a] : 0.0f;
+        b.gres[a] = dev->g_res[a];
+    }
+    b.gcells = dev->lb_grid ? dev->d_grid : nullptr;
+    b.gitems = dev->lb_grid ? dev->d_grid + dev->g_items_off : nullptr;
     b.trec = dev->lb_terms ? reinterpret_cast<const float4*>(reinterpret_cast<const uint32_t*>(dev->d_lbvh) +
                                                             dev->lb_term_off)
                            : nullptr;
@@ -2453,7 +2642,7 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
 }
 
 enum PathKind { kLanesLds, kLanesGlobal, kLanesBvh, kLanesBvhSpheres, kLanesBvh16, kLanesBvhSpheres16, kLanesTerms,
-                kLanesWideSpheres, kLanesWide, kLanesWideTerms, kJit, kInterpLds, kInterpGlobal };
+                kLanesWideSpheres, kLanesWide, kLanesWideTerms, kLanesGrid, kJit, kInterpLds, kInterpGlobal };
 
 template <bool kCount>
 static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
@@ -2478,6 +2667,8 @@ static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<8, kCount>, kBlock, dyn_lds);
     case kLanesWideTerms:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<9, kCount>, kBlock, dyn_lds);
+    case kLanesGrid:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<10, kCount>, kBlock, dyn_lds);
     case kInterpLds:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_kernel<true, kCount>, kBlock, dyn_lds);
     default:
@@ -2537,6 +2728,11 @@ static void static_launch(PathKind kind, dim3 grid, size_t dyn_lds, hipStream_t 
         break;
     case kLanesWideTerms:
         hipLaunchKernelGGL((pathtrace_lanes_kernel<9, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesGrid:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<10, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
                            dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
                            lane_bvh(dev));
         break;
@@ -2618,14 +2814,16 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
             // in LDS when it fits
             const size_t table = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
             if (dev->lb_root != kNoRef || dev->lb_always != 0u) {
-                if (dev->lb_wide)
+                if (dev->lb_grid)
+                    kind = kLanesGrid;
+                else if (dev->lb_wide)
                     kind = dev->lb_terms ? kLanesWideTerms : (dev->lb_spheres_only ? kLanesWideSpheres : kLanesWide);
                 else
                     kind = dev->lb_terms   ? kLanesTerms
                            : dev->lb_stack16 ? (dev->lb_spheres_only ? kLanesBvhSpheres16 : kLanesBvh16)
                                              : (dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh);
                 const size_t stacks = ((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u) + 15u) & ~(size_t)15u;
-                dyn_lds = stacks + (size_t)dev->lb_top * (dev->lb_wide ? 7u : 4u) * sizeof(float4);
+                dyn_lds = dev->lb_grid ? 0u : stacks + (size_t)dev->lb_top * (dev->lb_wide ? 7u : 4u) * sizeof(float4);
             } else {
                 kind = table <= kLanesLdsBudget ? kLanesLds : kLanesGlobal;
                 dyn_lds = kind == kLanesLds ? table : 0u;

@@ -477,13 +477,17 @@ def test_lanes_bvh_depth_bound(levels, monkeypatch):
     r.close()
 
 
-@pytest.mark.parametrize("scene", ["union90", "rtiow_cover", "csg32", "csg256_balanced", "deep600"])
-def test_lanes_wide_bvh_bitexact(scene, monkeypatch):
+@pytest.mark.parametrize("knob,scene", [("WOLOLO_LANES_WIDE", s) for s in
+                                        ["union90", "rtiow_cover", "csg32", "csg256_balanced", "deep600"]] +
+                         [("WOLOLO_LANES_GRID", s) for s in ["rtiow_cover", "deep600", "glass200"]])
+def test_lanes_wide_bvh_bitexact(knob, scene, monkeypatch):
     """4-wide lane BVH (WOLOLO_LANES_WIDE=1, lb_collapse4): spheres-only (rtiow), generic
     primitives (boxes, half-spaces: the union scene) and term mode (csg32, csg256 balanced),
     and the 600-sphere chain whose tree is as deep as the depth bound allows (its 16-bit
-    stack holds 3 entries per level); every image the oracle's bit for bit."""
-    monkeypatch.setenv("WOLOLO_LANES_WIDE", "1")
+    stack holds 3 entries per level); every image the oracle's bit for bit.  The same
+    scenes of single spheres through the uniform grid (WOLOLO_LANES_GRID=1, build_grid:
+    a DDA walk), and a cluster of overlapping glass spheres (rays that start inside)."""
+    monkeypatch.setenv(knob, "1")
     monkeypatch.setenv("WOLOLO_LANES_MIN_PRIMS", "64")
     if scene == "union90":
         r = _union_scene()
@@ -501,6 +505,22 @@ def test_lanes_wide_bvh_bitexact(scene, monkeypatch):
             items = nxt
         r.set_camera((-3.5, 0.5, 3.0), (0.0, 0.0, -1.0), (0, 1, 0), 60.0)
         p = wl.render_params(64, 40, spp=2, max_depth=6, mode=wl.MODE_PATHTRACE, seed=7)
+    elif scene == "glass200":
+        r = wl.Renderer("glass", max_nodes=1024)
+        rng = np.random.default_rng(11)
+        glass, clay = r.dielectric(1.5), r.lambertian((0.6, 0.5, 0.4))
+        items = []
+        for i in range(200):
+            sph = r.sphere(float(rng.uniform(0.15, 0.6)))
+            r.set_material(sph, glass if i % 2 else clay)
+            items.append(wl.arg(sph, tuple(float(v) for v in (rng.uniform(-2, 2), rng.uniform(-1, 1), rng.uniform(-4, 0)))))
+        while len(items) > 1:
+            nxt = [wl.arg(r.union(items[i], items[i + 1])) for i in range(0, len(items) - 1, 2)]
+            if len(items) % 2:
+                nxt.append(items[-1])
+            items = nxt
+        r.set_camera((0.0, 0.0, 3.0), (0.0, 0.0, -2.0), (0, 1, 0), 60.0)
+        p = wl.render_params(64, 48, spp=4, max_depth=8, mode=wl.MODE_PATHTRACE, seed=5)
     else:
         r, info = _scene(scene, "lanes")
         p = info.params(width=96, height=54, spp=8, seed=7)
@@ -512,7 +532,8 @@ def test_lanes_wide_bvh_bitexact(scene, monkeypatch):
         ref, _ = _oracle_rows(r, p)
         _cmp(img, ref, f"wide {scene} mode={mode}")
     info = r.lanes_info()
-    assert info["depth"] % 3 == 0 and info["depth"] <= 3 * 24, info  # 3 stack entries per 4-wide level
+    if knob == "WOLOLO_LANES_WIDE":
+        assert info["depth"] % 3 == 0 and info["depth"] <= 3 * 24, info  # 3 stack entries per 4-wide level
     r.close()
 
 
@@ -559,6 +580,7 @@ def test_jit_event_windows(window, monkeypatch):
     {"WOLOLO_JIT_TERMS": "1"},  # term transitions on csg256 balanced too (by default <= 64 primitives)
     {"WOLOLO_JIT_TERMS": "0"},  # the event-list form on csg32
     {"WOLOLO_JIT_TERMS": "1", "WOLOLO_JIT_DIST_CULL": "1"},  # groups beyond every lane's best skipped
+    {"WOLOLO_JIT_TERMS": "1", "WOLOLO_JIT_TERM_DIST": "1", "WOLOLO_JIT_KEY_VMOV": "1"},  # terms beyond a lane's best
 ])
 def test_jit_culling_knobs(knobs, monkeypatch):
     """The wave-level member skip, the bound-around-a-lone-primitive rule, the
