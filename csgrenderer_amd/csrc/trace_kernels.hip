@@ -327,6 +327,10 @@ constexpr uint32_t kLaneDepthMax = 24;
 #define WO_LANES_WIDE_DEFAULT 0
 #endif
 constexpr bool kLanesWideDefault = WO_LANES_WIDE_DEFAULT != 0;  // WOLOLO_LANES_WIDE overrides
+#ifndef WO_LANES_DYN_DEFAULT
+#define WO_LANES_DYN_DEFAULT 0
+#endif
+constexpr bool kLanesDynDefault = WO_LANES_DYN_DEFAULT != 0;  // WOLOLO_LANES_DYN overrides
 #ifndef WO_LANES_FUSED_SPHERE
 #define WO_LANES_FUSED_SPHERE 1
 #endif
@@ -357,9 +361,13 @@ __device__ __forceinline__ float box_near(float4 lo, float4 hi, F3 ri, F3 oi, fl
 // conjunctions (extract_terms: the leaves and the always list hold terms);
 // 7 / 8 / 9 = 3 / 2 / 6 over a 4-wide tree (lb_collapse4: four child boxes per
 // node, half the dependent node loads of a walk), always with 16-bit stacks.
-template <int kMode, bool kCountT>
+// 11 / 12 / 13 = 3 / 2 / 6 with the resumable walk (trace_step, dynamic ray fetch).
+template <int kModeT, bool kCountT>
 struct LaneTracer {
     static constexpr bool kCount = kCountT;
+    static constexpr bool kDyn = kModeT >= 11;
+    static constexpr bool kResumable = kDyn;
+    static constexpr int kMode = kModeT == 11 ? 3 : kModeT == 12 ? 2 : kModeT == 13 ? 6 : kModeT;
     static constexpr bool kBvh = kMode >= 2;
     static constexpr bool kWide = kMode >= 7 && kMode <= 9;
     static constexpr bool kGrid = kMode == 10;
@@ -503,25 +511,31 @@ struct LaneTracer {
         }
     }
 
-    // The smallest event key > `after` (entries and exits after t_min), or
-    // kEmptyKey; `inside` (first query only) counts the primitives whose
-    // interval holds t_min.  Boxes are pruned beyond the best event so far; the
-    // boxes holding the ray's start never are, so the count is complete.
-    // `up`: the count of true members (primitives; terms in term mode) rises at
-    // the returned key.
-    __device__ __forceinline__ uint64_t query(F3 o, F3 d, F3 ri, F3 oi, uint64_t after, uint32_t& inside, bool& up,
-                                              F3& inv, bool& have_inv) {
+    // One query's walk state (query / trace_step): the smallest event key > `after`
+    // found so far, whether the count rises there (term mode), the node to visit
+    // next and the lane stack's depth, the primitives (terms) holding t_min met so
+    // far, and the re-query's lower box bound.
+    struct QState {
+        uint64_t best, after;
+        uint32_t cur, sp, cnt;
+        float tlo;
+        bool up;
+    };
+
+    // A leaf of the walk (or of the always list / a grid cell): a primitive, or in
+    // term mode a term.  Term mode: a term (a conjunction of one or two literals,
+    // each a primitive or its complement) changes value only at an event of a
+    // literal X, and then exactly when the other literal holds at that key; it
+    // rises where X's literal becomes true (X's entry for a positive literal, its
+    // exit for a complement).  A primitive is in one term, so one key changes one term.
+    __device__ __forceinline__ void visit_leaf(uint32_t ref, uint32_t& cnt, QState& s, F3 o, F3 d, F3& inv,
+                                               bool& have_inv) {
         const float tmin = WO_T_MIN;
-        uint64_t best = kEmptyKey;
-        bool best_up = false;
-        // Term mode: a term (a conjunction of one or two literals, each a primitive or
-        // its complement) changes value only at an event of a literal X, and then
-        // exactly when the other literal holds at that key; it rises where X's
-        // literal becomes true (X's entry for a positive literal, its exit for a
-        // complement).  A primitive is in one term, so one key changes one term.
-        auto visit_term = [&](uint32_t ti, uint32_t& cnt) {
+        uint64_t& best = s.best;
+        const uint64_t after = s.after;
+        if constexpr (kTerms) {
             // the record's header and both literals' inline spheres: independent loads
-            const float4* rec = ltrec + kTermRecF4 * ti;
+            const float4* rec = ltrec + kTermRecF4 * ref;
             const float4 hd = rec[0];
             const uint2 tl = make_uint2(__float_as_uint(hd.x), __float_as_uint(hd.y));
             const uint32_t kinds = __float_as_uint(hd.z);
@@ -570,181 +584,204 @@ struct LaneTracer {
                 const bool ti = has & (ei != 0ull) & (ei > after) & (ei < best) & (one | lit_at(y, ei));
                 WO_WK_N(WO_WORK_EVENTS, ti ? 1u : 0u);
                 best = ti ? ei : best;
-                best_up = ti ? pos[x] : best_up;
+                s.up = ti ? pos[x] : s.up;
                 const bool to = has & (eo != kEmptyKey) & (eo > after) & (eo < best) & (one | lit_at(y, eo));
                 WO_WK_N(WO_WORK_EVENTS, to ? 1u : 0u);
                 best = to ? eo : best;
-                best_up = to ? !pos[x] : best_up;
+                s.up = to ? !pos[x] : s.up;
             }
-        };
-        auto visit = [&](uint32_t ord, uint32_t& cnt) {
+            return;
+        }
+        const uint32_t ord = ref;
 #if WO_LANES_FUSED_SPHERE
-            if constexpr (kSpheresOnly) {
-                // a sphere's interval [-b - s, -b + s] exists exactly when disc >= 0: the
-                // count and the events inside the sqrt branch, no empty interval formed
-                // (the specialised kernel's lone spheres; same bits as prim_ivl's form)
-                WO_WK(WO_WORK_SPHERE_TESTS);
-                const float4 g = lgeo[ord];
-                float b, ll;
-                sphere_bl(g.x, g.y, g.z, o, d, b, ll);
-                const float disc = g.w - ll;
-                if (__ballot(sphere_need(b, disc)) != 0ull) {
-                    asm volatile("");
-                    if (!(disc < 0.0f)) {
-                        const float s = sqrt_pt(disc), nb = -b, la = nb - s, lb = nb + s;
-                        if ((la <= tmin) & (lb > tmin)) ++cnt;
-                        const uint64_t k0 = event_key(la, ord, 0u, 0u), k1 = event_key(lb, ord, 1u, 0u);
-                        if ((la > tmin) & (k0 > after)) {
-                            WO_WK(WO_WORK_EVENTS);
-                            best = k0 < best ? k0 : best;
-                        }
-                        if ((lb > tmin) & (lb < kInf) & (k1 > after)) {
-                            WO_WK(WO_WORK_EVENTS);
-                            best = k1 < best ? k1 : best;
-                        }
+        if constexpr (kSpheresOnly) {
+            // a sphere's interval [-b - s, -b + s] exists exactly when disc >= 0: the
+            // count and the events inside the sqrt branch, no empty interval formed
+            // (the specialised kernel's lone spheres; same bits as prim_ivl's form)
+            WO_WK(WO_WORK_SPHERE_TESTS);
+            const float4 g = lgeo[ord];
+            float b, ll;
+            sphere_bl(g.x, g.y, g.z, o, d, b, ll);
+            const float disc = g.w - ll;
+            if (__ballot(sphere_need(b, disc)) != 0ull) {
+                asm volatile("");
+                if (!(disc < 0.0f)) {
+                    const float s = sqrt_pt(disc), nb = -b, la = nb - s, lb = nb + s;
+                    if ((la <= tmin) & (lb > tmin)) ++cnt;
+                    const uint64_t k0 = event_key(la, ord, 0u, 0u), k1 = event_key(lb, ord, 1u, 0u);
+                    if ((la > tmin) & (k0 > after)) {
+                        WO_WK(WO_WORK_EVENTS);
+                        best = k0 < best ? k0 : best;
+                    }
+                    if ((lb > tmin) & (lb < kInf) & (k1 > after)) {
+                        WO_WK(WO_WORK_EVENTS);
+                        best = k1 < best ? k1 : best;
                     }
                 }
-                return;
             }
+            return;
+        }
 #endif
-            const Ivl iv = prim_ivl(ord, o, d, inv, have_inv);
-            if (!(iv.a > iv.b)) {
-                if ((iv.a <= tmin) & (iv.b > tmin)) ++cnt;
-                const uint64_t k0 = event_key(iv.a, ord, 0u, iv.ma), k1 = event_key(iv.b, ord, 1u, iv.mb);
-                if ((iv.a > tmin) & (k0 > after)) {
-                    WO_WK(WO_WORK_EVENTS);
-                    best = k0 < best ? k0 : best;
-                }
-                if ((iv.b > tmin) & (iv.b < kInf) & (k1 > after)) {
-                    WO_WK(WO_WORK_EVENTS);
-                    best = k1 < best ? k1 : best;
-                }
+        const Ivl iv = prim_ivl(ord, o, d, inv, have_inv);
+        if (!(iv.a > iv.b)) {
+            if ((iv.a <= tmin) & (iv.b > tmin)) ++cnt;
+            const uint64_t k0 = event_key(iv.a, ord, 0u, iv.ma), k1 = event_key(iv.b, ord, 1u, iv.mb);
+            if ((iv.a > tmin) & (k0 > after)) {
+                WO_WK(WO_WORK_EVENTS);
+                best = k0 < best ? k0 : best;
             }
-        };
-        auto leaf = [&](uint32_t ref, uint32_t& cnt) {
-            if constexpr (kTerms)
-                visit_term(ref, cnt);
-            else
-                visit(ref, cnt);
-        };
-        uint32_t in_always = 0, in_tree = 0;
-        for (uint32_t i = 0; i < nalways; ++i) leaf(lkind[nprims + i], in_always);
-        if constexpr (kGrid) {
-            grid_walk(o, d, ri, oi, after, best, in_tree, visit);
-            inside = in_always + in_tree;
-            up = !(best & kKeyTypeBit);
-            return best;
+            if ((iv.b > tmin) & (iv.b < kInf) & (k1 > after)) {
+                WO_WK(WO_WORK_EVENTS);
+                best = k1 < best ? k1 : best;
+            }
         }
-        // a re-query (after != 0) prunes boxes that end before the last key: their
-        // events all lie at or before it (the boxes' slack covers the slab test's
-        // rounding; the margin below covers the key's own t).  The first query
-        // keeps every box that holds the ray's start (the count at t_min).
+    }
+
+    // A query's start: the always list, then the walk from the root.  A re-query
+    // (after != 0) prunes boxes that end before the last key: their events all lie
+    // at or before it (the boxes' slack covers the slab test's rounding; the
+    // margin below covers the key's own t).  The first query keeps every box that
+    // holds the ray's start (the count at t_min).
+    __device__ __forceinline__ void qbegin(QState& s, uint64_t after, F3 o, F3 d, F3& inv, bool& have_inv) {
+        s.best = kEmptyKey;
+        s.after = after;
+        s.up = false;
+        s.cnt = 0;
+        for (uint32_t i = 0; i < nalways; ++i) visit_leaf(lkind[nprims + i], s.cnt, s, o, d, inv, have_inv);
         const float tafter = after == 0ull ? 0.0f : __uint_as_float((uint32_t)(after >> 32));
-        const float tlo = fmaxf(__builtin_fmaf(-2e-5f, tafter, tafter) - 1e-6f, 0.0f);
-        uint32_t cur = lroot, sp = 0;
-        while (cur != kNoRef) {
-            WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);  // lane tracer: walk trips per wave
-            if (cur & kLeafRef) {
-                leaf(cur & ~kLeafRef, in_tree);
-                cur = kNoRef;
-            } else if constexpr (kWide) {
-                // four children: lo.x, hi.x, lo.y, hi.y, lo.z, hi.z of each, then the refs
-                WO_WK_N(WO_WORK_BOUND_TESTS, 4u);
-                float4 q[7];
-                if (cur < ntop) {
-                    const LdsNodes nd = ltop + 7u * cur;
+        s.tlo = fmaxf(__builtin_fmaf(-2e-5f, tafter, tafter) - 1e-6f, 0.0f);
+        s.cur = lroot;
+        s.sp = 0;
+    }
+
+    // One trip of the walk: a leaf, or a node (its children's boxes, nearest hit
+    // child next, the other(s) pushed); then a pop when the walk has no next node.
+    __device__ __forceinline__ void trip(QState& s, F3 o, F3 d, F3 ri, F3 oi, F3& inv, bool& have_inv) {
+        WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);  // lane tracer: walk trips per wave
+        uint32_t cur = s.cur, sp = s.sp;
+        const float tlo = s.tlo;
+        if (cur & kLeafRef) {
+            visit_leaf(cur & ~kLeafRef, s.cnt, s, o, d, inv, have_inv);
+            cur = kNoRef;
+        } else if constexpr (kWide) {
+            // four children: lo.x, hi.x, lo.y, hi.y, lo.z, hi.z of each, then the refs
+            WO_WK_N(WO_WORK_BOUND_TESTS, 4u);
+            float4 q[7];
+            if (cur < ntop) {
+                const LdsNodes nd = ltop + 7u * cur;
 #pragma unroll
-                    for (int k = 0; k < 7; ++k) q[k] = nd[k];
-                    asm volatile("");
-                } else {
-                    const GlobalNodes nd = (GlobalNodes)lnodes + 7u * cur;
-#pragma unroll
-                    for (int k = 0; k < 7; ++k) q[k] = nd[k];
-                }
-                const float tb = best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(best >> 32));
-                // per child a sort key: the top 16 bits of max(near, 0) (monotone as an
-                // unsigned integer; the order only steers the walk) | the child's 16-bit
-                // ref; ~0 for a miss or an empty slot
-                uint32_t kk[4];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float ax = __builtin_fmaf(f4c(q[0], c), ri.x, -oi.x), bx = __builtin_fmaf(f4c(q[1], c), ri.x, -oi.x);
-                    const float ay = __builtin_fmaf(f4c(q[2], c), ri.y, -oi.y), by = __builtin_fmaf(f4c(q[3], c), ri.y, -oi.y);
-                    const float az = __builtin_fmaf(f4c(q[4], c), ri.z, -oi.z), bz = __builtin_fmaf(f4c(q[5], c), ri.z, -oi.z);
-                    const float n = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-                    const float f = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-                    const uint32_t r16 = __float_as_uint(f4c(q[6], c));
-                    const float n0 = fmaxf(n, 0.0f);
-                    const bool h = (f >= fmaxf(n0, tlo)) & (n <= tb) & (r16 != kNoRef16);
-                    kk[c] = h ? ((__float_as_uint(n0) & 0xffff0000u) | r16) : 0xffffffffu;
-                }
-                // nearest first: a 4-key sorting network (misses sort last)
-                auto ce = [&](int i, int j) {
-                    const uint32_t lo = kk[i] < kk[j] ? kk[i] : kk[j], hi = kk[i] < kk[j] ? kk[j] : kk[i];
-                    kk[i] = lo;
-                    kk[j] = hi;
-                };
-                ce(0, 1);
-                ce(2, 3);
-                ce(0, 2);
-                ce(1, 3);
-                ce(1, 2);
-                cur = kk[0] == 0xffffffffu ? kNoRef : (kk[0] & 0x7fffu) | ((kk[0] & 0x8000u) << 16);
-                // the farther ones on the stack, farthest deepest (sp < 3 x the tree's levels)
-#pragma unroll
-                for (int c = 3; c >= 1; --c) {
-                    if (kk[c] != 0xffffffffu) {
-                        stk16[sp * kBlock] = (uint16_t)kk[c];
-                        ++sp;
-                    }
-                }
+                for (int k = 0; k < 7; ++k) q[k] = nd[k];
+                asm volatile("");
             } else {
-                WO_WK_N(WO_WORK_BOUND_TESTS, 2u);
-                float4 a0, a1, b0, b1;
-                if (cur < ntop) {  // the top levels: LDS latency instead of a cache round trip
-                    const LdsNodes nd = ltop + 4u * cur;
-                    a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
-                    asm volatile("");  // the branches' tails differ: the loads are not merged into flat loads
-                } else {
-                    const GlobalNodes nd = (GlobalNodes)lnodes + 4u * cur;
-                    a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
-                }
-                // useful range: up to the best event so far
-                const float tb = best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(best >> 32));
-                float fa, fb;
-                const float na = box_near(a0, a1, ri, oi, fa), nb = box_near(b0, b1, ri, oi, fb);
-                const bool ha = (fa >= fmaxf(na, tlo)) & (na <= tb);
-                const bool hb = (fb >= fmaxf(nb, tlo)) & (nb <= tb);
-                const uint32_t ra = __float_as_uint(a0.w), rb = __float_as_uint(a1.w);
-                if (ha & hb) {
-                    const bool a_first = na <= nb;
-                    cur = a_first ? ra : rb;
-                    const uint32_t other = a_first ? rb : ra;
-                    if constexpr (kStack16)  // refs < 2^15 (build_lbvh): the leaf flag moves to bit 15
-                        stk16[sp * kBlock] = (uint16_t)((other & 0x7fffu) | ((other >> 16) & 0x8000u));
-                    else
-                        stk[sp * kBlock] = other;  // sp < the tree's depth (build_lbvh)
+                const GlobalNodes nd = (GlobalNodes)lnodes + 7u * cur;
+#pragma unroll
+                for (int k = 0; k < 7; ++k) q[k] = nd[k];
+            }
+            const float tb = s.best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(s.best >> 32));
+            // per child a sort key: the top 16 bits of max(near, 0) (monotone as an
+            // unsigned integer; the order only steers the walk) | the child's 16-bit
+            // ref; ~0 for a miss or an empty slot
+            uint32_t kk[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float ax = __builtin_fmaf(f4c(q[0], c), ri.x, -oi.x), bx = __builtin_fmaf(f4c(q[1], c), ri.x, -oi.x);
+                const float ay = __builtin_fmaf(f4c(q[2], c), ri.y, -oi.y), by = __builtin_fmaf(f4c(q[3], c), ri.y, -oi.y);
+                const float az = __builtin_fmaf(f4c(q[4], c), ri.z, -oi.z), bz = __builtin_fmaf(f4c(q[5], c), ri.z, -oi.z);
+                const float n = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                const float f = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                const uint32_t r16 = __float_as_uint(f4c(q[6], c));
+                const float n0 = fmaxf(n, 0.0f);
+                const bool h = (f >= fmaxf(n0, tlo)) & (n <= tb) & (r16 != kNoRef16);
+                kk[c] = h ? ((__float_as_uint(n0) & 0xffff0000u) | r16) : 0xffffffffu;
+            }
+            // nearest first: a 4-key sorting network (misses sort last)
+            auto ce = [&](int i, int j) {
+                const uint32_t lo = kk[i] < kk[j] ? kk[i] : kk[j], hi = kk[i] < kk[j] ? kk[j] : kk[i];
+                kk[i] = lo;
+                kk[j] = hi;
+            };
+            ce(0, 1);
+            ce(2, 3);
+            ce(0, 2);
+            ce(1, 3);
+            ce(1, 2);
+            cur = kk[0] == 0xffffffffu ? kNoRef : (kk[0] & 0x7fffu) | ((kk[0] & 0x8000u) << 16);
+            // the farther ones on the stack, farthest deepest (sp < 3 x the tree's levels)
+#pragma unroll
+            for (int c = 3; c >= 1; --c) {
+                if (kk[c] != 0xffffffffu) {
+                    stk16[sp * kBlock] = (uint16_t)kk[c];
                     ++sp;
-                } else {
-                    cur = ha ? ra : (hb ? rb : kNoRef);
                 }
             }
-            if ((cur == kNoRef) & (sp != 0u)) {
-                --sp;
-                if constexpr (kStack16) {
-                    const uint32_t e = stk16[sp * kBlock];
-                    cur = (e & 0x7fffu) | ((e & 0x8000u) << 16);
-                } else {
-                    cur = stk[sp * kBlock];
-                }
+        } else {
+            WO_WK_N(WO_WORK_BOUND_TESTS, 2u);
+            float4 a0, a1, b0, b1;
+            if (cur < ntop) {  // the top levels: LDS latency instead of a cache round trip
+                const LdsNodes nd = ltop + 4u * cur;
+                a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                asm volatile("");  // the branches' tails differ: the loads are not merged into flat loads
+            } else {
+                const GlobalNodes nd = (GlobalNodes)lnodes + 4u * cur;
+                a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+            }
+            // useful range: up to the best event so far
+            const float tb = s.best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(s.best >> 32));
+            float fa, fb;
+            const float na = box_near(a0, a1, ri, oi, fa), nb = box_near(b0, b1, ri, oi, fb);
+            const bool ha = (fa >= fmaxf(na, tlo)) & (na <= tb);
+            const bool hb = (fb >= fmaxf(nb, tlo)) & (nb <= tb);
+            const uint32_t ra = __float_as_uint(a0.w), rb = __float_as_uint(a1.w);
+            if (ha & hb) {
+                const bool a_first = na <= nb;
+                cur = a_first ? ra : rb;
+                const uint32_t other = a_first ? rb : ra;
+                if constexpr (kStack16)  // refs < 2^15 (build_lbvh): the leaf flag moves to bit 15
+                    stk16[sp * kBlock] = (uint16_t)((other & 0x7fffu) | ((other >> 16) & 0x8000u));
+                else
+                    stk[sp * kBlock] = other;  // sp < the tree's depth (build_lbvh)
+                ++sp;
+            } else {
+                cur = ha ? ra : (hb ? rb : kNoRef);
             }
         }
-        inside = in_always + in_tree;
+        if ((cur == kNoRef) & (sp != 0u)) {
+            --sp;
+            if constexpr (kStack16) {
+                const uint32_t e = stk16[sp * kBlock];
+                cur = (e & 0x7fffu) | ((e & 0x8000u) << 16);
+            } else {
+                cur = stk[sp * kBlock];
+            }
+        }
+        s.cur = cur;
+        s.sp = sp;
+    }
+
+    // The smallest event key > `after` (entries and exits after t_min), or
+    // kEmptyKey; `inside` (first query only) counts the primitives whose
+    // interval holds t_min.  Boxes are pruned beyond the best event so far; the
+    // boxes holding the ray's start never are, so the count is complete.
+    // `up`: the count of true members (primitives; terms in term mode) rises at
+    // the returned key.
+    __device__ __forceinline__ uint64_t query(F3 o, F3 d, F3 ri, F3 oi, uint64_t after, uint32_t& inside, bool& up,
+                                              F3& inv, bool& have_inv) {
+        QState s;
+        qbegin(s, after, o, d, inv, have_inv);
+        if constexpr (kGrid) {
+            auto visit = [&](uint32_t ord, uint32_t& cnt) { visit_leaf(ord, cnt, s, o, d, inv, have_inv); };
+            grid_walk(o, d, ri, oi, after, s.best, s.cnt, visit);
+            inside = s.cnt;
+            up = !(s.best & kKeyTypeBit);
+            return s.best;
+        }
+        while (s.cur != kNoRef) trip(s, o, d, ri, oi, inv, have_inv);
+        inside = s.cnt;
         if constexpr (kTerms)
-            up = best_up;
+            up = s.up;
         else  // a primitive's count rises at its entry
-            up = !(best & kKeyTypeBit);
-        return best;
+            up = !(s.best & kKeyTypeBit);
+        return s.best;
     }
 
     // Events in key order, one query each, from the count of primitives holding
@@ -775,6 +812,69 @@ struct LaneTracer {
             key = query(o, d, ri, oi, key, unused, up, inv, have_inv);
         }
         return false;
+    }
+
+    // Resumable trace (kDyn, pathtrace_block's dynamic ray fetch): the walk of a
+    // query carries over between calls in `dq`, so a wave whose lanes' walks end
+    // at different trips need not run its slowest lane's walk to the end before
+    // the finished lanes shade and take their next rays.  Once at most
+    // WO_LANES_DYN_WALKERS lanes are still walking (and `may_bail`: the tile's
+    // queue still has jobs, so the finished lanes have work to fetch), the walking
+    // lanes return kTracePending after a trip and resume from the same state at
+    // the next call.  Each call makes at least one trip, so every walk finishes.
+    // Same queries, same keys: the hit is trace_ordered's bit for bit.
+    QState dq;
+    uint32_t dyn_walkers;  // bail-out threshold (LaneBvh::dyn_walkers, wave-uniform)
+    uint32_t dcnt;   // the count of true members at the last key processed
+    bool droot;      // the root's value at t_min
+    bool dfirst;     // the walk in dq is the ray's first query
+    bool dpending;   // a walk is in dq (set up by an earlier call)
+    __device__ __forceinline__ int trace_step(F3 o, F3 d, Hit& hit, bool may_bail) {
+        const float dx = fabsf(d.x) < 1e-30f ? copysignf(1e-30f, d.x) : d.x;
+        const float dy = fabsf(d.y) < 1e-30f ? copysignf(1e-30f, d.y) : d.y;
+        const float dz = fabsf(d.z) < 1e-30f ? copysignf(1e-30f, d.z) : d.z;
+        const F3 ri = f3(__builtin_amdgcn_rcpf(dx), __builtin_amdgcn_rcpf(dy), __builtin_amdgcn_rcpf(dz));
+        const F3 oi = f3(o.x * ri.x, o.y * ri.y, o.z * ri.z);
+        // the exact reciprocal (generic primitives' axis half-spaces) on first need
+        // in this call: the same values whenever it is recomputed
+        F3 inv = f3(0.0f, 0.0f, 0.0f);
+        bool have_inv = false;
+        if (!dpending) {
+            qbegin(dq, 0ull, o, d, inv, have_inv);
+            dfirst = true;
+        }
+        for (;;) {
+            bool walked = false;
+            while (dq.cur != kNoRef) {
+                if (walked && may_bail && (uint32_t)__popcll(__ballot(true)) <= dyn_walkers) {
+                    dpending = true;
+                    return kTracePending;
+                }
+                trip(dq, o, d, ri, oi, inv, have_inv);
+                walked = true;
+            }
+            const uint64_t key = dq.best;
+            const bool up = kTerms ? dq.up : !(key & kKeyTypeBit);
+            if (dfirst) {
+                dcnt = dq.cnt;
+                droot = dcnt > 0u;
+                dfirst = false;
+            }
+            if (key == kEmptyKey) {
+                dpending = false;
+                return kTraceMiss;
+            }
+            WO_WK(WO_WORK_SWEEP_STEPS);
+            dcnt = up ? dcnt + 1u : dcnt - 1u;
+            const bool rv = dcnt > 0u;
+            if (rv != droot) {
+                hit_from_key(key, rv ? 1u : 0u, hit);
+                dpending = false;
+                return kTraceHit;
+            }
+            WO_WK(WO_WORK_RECOLLECTS);
+            qbegin(dq, key, o, d, inv, have_inv);
+        }
     }
 
     __device__ __forceinline__ bool trace(F3 o, F3 d, Hit& hit) {
@@ -910,6 +1010,7 @@ struct LaneBvh {
     uint32_t nalways, root, nprims;
     uint32_t depth;        // internal levels of the tree: the lane stack's entries
     uint32_t ntop;         // nodes [0, ntop) staged in LDS after the lane stacks
+    uint32_t dyn_walkers;  // resumable walk: walking lanes at which a wave bails out (WOLOLO_LANES_DYN_WALKERS)
     float glo[3], gh[3], ginv[3];  // uniform grid (kMode 10): origin, cell size, 1 / cell size
     uint32_t gres[3];
     const uint32_t* gcells;        // ncells + 1 offsets into gitems
@@ -925,14 +1026,23 @@ template <int kMode, bool kCount>
 #ifndef WO_LANES_TERMS_MIN_WAVES
 #define WO_LANES_TERMS_MIN_WAVES 7  // csg512_balanced: 80.8 ms at 7 (13 VGPRs spilled), 82.0 at 6 (none)
 #endif
-__global__ __launch_bounds__(kBlock, (kMode == 6 || kMode == 9) ? WO_LANES_TERMS_MIN_WAVES
+#ifndef WO_LANES_DYN_MIN_WAVES
+#define WO_LANES_DYN_MIN_WAVES 7
+#endif
+#ifndef WO_LANES_DYN_TERMS_MIN_WAVES
+#define WO_LANES_DYN_TERMS_MIN_WAVES 6  // csg512_balanced: 56.4 ms at 6 (no spill), 57.2 at 7 (31 VGPRs spilled)
+#endif
+__global__ __launch_bounds__(kBlock, kMode == 13 ? WO_LANES_DYN_TERMS_MIN_WAVES
+                                    : kMode >= 11 ? WO_LANES_DYN_MIN_WAVES
+                                    : (kMode == 6 || kMode == 9) ? WO_LANES_TERMS_MIN_WAVES
                                     : (kMode == 2 || kMode == 4 || kMode == 7 || kMode == 8) ? WO_LANES_BVH_MIN_WAVES
                                                                                : WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
     const WoRec* __restrict__ prog, const float4* __restrict__ gnodes, const uint32_t* __restrict__ ordpc,
     const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t ntrav, uint32_t local_rows, float4* __restrict__ out,
     unsigned long long* __restrict__ seg_slots, PathLaunch tg, LaneBvh bvh) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    constexpr bool kLds = kMode == 0;
+    constexpr int kBase = LaneTracer<kMode, kCount>::kMode;  // the walk's form (11 / 12 / 13: resumable 3 / 2 / 6)
+    constexpr bool kLds = kBase == 0;
     LaneTracer<kMode, kCount> tr;
     tr.prog = prog;
     tr.ordpc = ordpc;
@@ -953,11 +1063,15 @@ __global__ __launch_bounds__(kBlock, (kMode == 6 || kMode == 9) ? WO_LANES_TERMS
     tr.nalways = bvh.nalways;
     tr.lroot = bvh.root;
     tr.nprims = bvh.nprims;
-    tr.stk = smem + threadIdx.x;  // kMode >= 2 only
+    tr.stk = smem + threadIdx.x;  // kBase >= 2 only
     tr.stk16 = reinterpret_cast<uint16_t*>(smem) + threadIdx.x;
     tr.ntop = 0;
     tr.ltop = (typename LaneTracer<kMode, kCount>::LdsNodes)nullptr;
-    if constexpr (kMode >= 2) {
+    if constexpr (LaneTracer<kMode, kCount>::kDyn) {
+        tr.dpending = false;
+        tr.dyn_walkers = bvh.dyn_walkers;
+    }
+    if constexpr (kBase >= 2) {
         // the top levels of the BVH next to the stacks; pathtrace_block's first
         // barrier orders the copy before any walk
         constexpr bool kStack16 = LaneTracer<kMode, kCount>::kStack16;
@@ -1258,6 +1372,7 @@ struct WoDev {
     size_t grid_cap;
     uint32_t g_items_off;
     uint32_t lb_terms;     // term mode (kMode 6): terms the BVH's leaves and always list refer to
+    uint32_t last_kind;    // the PathKind of the last path launch (wo_dev_lanes_info)
     uint32_t lb_term_off;  // their records (kTermRecF4 float4 each) at this u32 offset of d_lbvh
     uint32_t lb_top;       // nodes staged in LDS per workgroup
     uint32_t lb_depth;     // internal levels of the lane BVH (<= kLaneDepthMax)
@@ -2092,12 +2207,13 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
         if (levels > kLaneDepthMax) levels = kLaneDepthMax;
         LbBox root_box;
         dev->lb_root = lb_build(prims, 0u, (uint32_t)prims.size(), levels, nodes, root_box, dev->lb_depth);
-        // 4-wide nodes (WOLOLO_LANES_WIDE=1): refs must fit the 16-bit stack entries
-        // default: term mode over more than 256 terms (csg512_balanced 82.0 -> 70.5 ms;
-        // neutral on csg256 balanced's 65 terms, 16.4 / 16.5 ms; slower on csg32's 14,
-        // 8.9 -> 9.6, and on the RTIOW cover's spheres, 11.7 -> 13.7)
+        // 4-wide nodes (WOLOLO_LANES_WIDE=1): refs must fit the 16-bit stack entries.
+        // Off by default: csg512_balanced 82.0 -> 70.5 ms over the binary walk, but the
+        // binary resumable walk (kLanesDynTerms, the default there) takes 56.4; neutral
+        // on csg256 balanced's 65 terms, 16.4 / 16.5 ms; slower on csg32's 14, 8.9 ->
+        // 9.6, and on the RTIOW cover's spheres, 11.7 -> 13.7
         const char* wv = getenv("WOLOLO_LANES_WIDE");
-        const bool want_wide = wv && *wv ? wv[0] == '1' : (kLanesWideDefault || terms.size() > 256u);
+        const bool want_wide = wv && *wv ? wv[0] == '1' : kLanesWideDefault;
         const uint32_t nrefs = terms.empty() ? n_prims : (uint32_t)terms.size();
         if (want_wide && !(dev->lb_root & kLeafRef) && nrefs < 0x8000u) {
             std::vector<float4> n4;
@@ -2195,6 +2311,9 @@ static LaneBvh lane_bvh(const WoDev* dev) {
     b.nprims = dev->lb_nprims;
     b.ntop = dev->lb_top;
     b.depth = dev->lb_depth;
+    b.dyn_walkers = 24u;  // measured: tools/env_ab.sh rtiow_cover
+    if (const char* v = getenv("WOLOLO_LANES_DYN_WALKERS"))
+        if (*v) b.dyn_walkers = (uint32_t)strtoul(v, NULL, 10);
     for (int a = 0; a < 3; ++a) {
         b.glo[a] = dev->g_lo[a];
         b.gh[a] = dev->g_h[a];
@@ -2544,6 +2663,7 @@ extern "C" int wo_dev_lanes_info(WoDev* dev, uint32_t* out) {
     out[1] = dev->lb_depth;
     out[2] = dev->lb_top;
     out[3] = dev->lb_always;
+    out[4] = dev->last_kind;
     return 0;
 }
 
@@ -2642,7 +2762,8 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
 }
 
 enum PathKind { kLanesLds, kLanesGlobal, kLanesBvh, kLanesBvhSpheres, kLanesBvh16, kLanesBvhSpheres16, kLanesTerms,
-                kLanesWideSpheres, kLanesWide, kLanesWideTerms, kLanesGrid, kJit, kInterpLds, kInterpGlobal };
+                kLanesWideSpheres, kLanesWide, kLanesWideTerms, kLanesGrid, kLanesDynSpheres, kLanesDyn, kLanesDynTerms,
+                kJit, kInterpLds, kInterpGlobal };
 
 template <bool kCount>
 static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
@@ -2669,6 +2790,12 @@ static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<9, kCount>, kBlock, dyn_lds);
     case kLanesGrid:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<10, kCount>, kBlock, dyn_lds);
+    case kLanesDynSpheres:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<11, kCount>, kBlock, dyn_lds);
+    case kLanesDyn:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<12, kCount>, kBlock, dyn_lds);
+    case kLanesDynTerms:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<13, kCount>, kBlock, dyn_lds);
     case kInterpLds:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_kernel<true, kCount>, kBlock, dyn_lds);
     default:
@@ -2733,6 +2860,21 @@ static void static_launch(PathKind kind, dim3 grid, size_t dyn_lds, hipStream_t 
         break;
     case kLanesGrid:
         hipLaunchKernelGGL((pathtrace_lanes_kernel<10, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesDynSpheres:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<11, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesDyn:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<12, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesDynTerms:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<13, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
                            dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
                            lane_bvh(dev));
         break;
@@ -2822,6 +2964,16 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
                     kind = dev->lb_terms   ? kLanesTerms
                            : dev->lb_stack16 ? (dev->lb_spheres_only ? kLanesBvhSpheres16 : kLanesBvh16)
                                              : (dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh);
+                // the resumable walk (dynamic ray fetch) for the binary 32-bit-stack forms:
+                // WOLOLO_LANES_DYN=1 (or 0) over the default, which is term mode over more
+                // than 256 terms (csg512_balanced 84.3 -> 56.4 ms; slower where walks are
+                // short or alike: the RTIOW cover 11.7 -> 12.9-15.5 ms, csg256 balanced's
+                // 65 terms 16.5 -> 18.2)
+                const char* dv = getenv("WOLOLO_LANES_DYN");
+                const bool dyn = dv && *dv ? dv[0] == '1' : (kLanesDynDefault || dev->lb_terms > 256u);
+                if (dyn && kind == kLanesBvhSpheres) kind = kLanesDynSpheres;
+                else if (dyn && kind == kLanesBvh) kind = kLanesDyn;
+                else if (dyn && kind == kLanesTerms) kind = kLanesDynTerms;
                 const size_t stacks = ((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u) + 15u) & ~(size_t)15u;
                 dyn_lds = dev->lb_grid ? 0u : stacks + (size_t)dev->lb_top * (dev->lb_wide ? 7u : 4u) * sizeof(float4);
             } else {
@@ -2849,6 +3001,7 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
                 return -1;
             }
         }
+        dev->last_kind = (uint32_t)kind;
         int per_cu = 0;
         hipFunction_t jfn = count ? dev->count_fn : dev->jit_fn;
         if (kind == kJit)

@@ -308,11 +308,12 @@ class Renderer:
         return (None if o < 0 else JIT_ORIGINS[o]), sec.value
 
     def lanes_info(self):
-        """The lane tracer's BVH: {"nodes", "depth", "top", "always"}, or None if not on the lane tracer."""
-        out = (c_uint32 * 4)()
+        """The lane tracer's BVH: {"nodes", "depth", "top", "always", "kind"} ("kind": the kernel
+        form of the last path launch, trace_kernels.hip PathKind), or None if not on the lane tracer."""
+        out = (c_uint32 * 5)()
         if self.lib.wo_renderer_lanes_info(self.ptr, out) < 0:
             return None
-        return dict(zip(("nodes", "depth", "top", "always"), list(out)))
+        return dict(zip(("nodes", "depth", "top", "always", "kind"), list(out)))
 
     def set_jit(self, mode: int):
         self.lib.wo_renderer_set_jit(self.ptr, int(mode))

@@ -154,7 +154,8 @@ def _oracle_rows(r, params):
 
 
 @pytest.mark.parametrize("path", PATHS)
-@pytest.mark.parametrize("scene", ["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain"])
+@pytest.mark.parametrize("scene", ["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain",
+                                   "csg512_balanced"])
 @pytest.mark.parametrize("mode", [wl.MODE_PATHTRACE, wl.MODE_NORMALS])
 def test_pathtrace_small_frame_bitexact(scene, mode, path):
     r, info = _scene(scene, path)
@@ -167,7 +168,8 @@ def test_pathtrace_small_frame_bitexact(scene, mode, path):
 
 
 @pytest.mark.parametrize("path", PATHS)
-@pytest.mark.parametrize("scene", ["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain"])
+@pytest.mark.parametrize("scene", ["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain",
+                                   "csg512_balanced"])
 def test_pathtrace_full_size_sampled_pixels(scene, path):
     """BASELINE configs at full size (1920x1080, 64 spp, 8 bounces): the whole frame on
     the GPU, a random sample of pixels on the oracle.  The lane tracer runs union-only
@@ -479,14 +481,19 @@ def test_lanes_bvh_depth_bound(levels, monkeypatch):
 
 @pytest.mark.parametrize("knob,scene", [("WOLOLO_LANES_WIDE", s) for s in
                                         ["union90", "rtiow_cover", "csg32", "csg256_balanced", "deep600"]] +
-                         [("WOLOLO_LANES_GRID", s) for s in ["rtiow_cover", "deep600", "glass200"]])
+                         [("WOLOLO_LANES_GRID", s) for s in ["rtiow_cover", "deep600", "glass200"]] +
+                         [("WOLOLO_LANES_DYN", s) for s in
+                          ["union90", "rtiow_cover", "csg32", "csg256_balanced", "deep600", "glass200"]])
 def test_lanes_wide_bvh_bitexact(knob, scene, monkeypatch):
     """4-wide lane BVH (WOLOLO_LANES_WIDE=1, lb_collapse4): spheres-only (rtiow), generic
     primitives (boxes, half-spaces: the union scene) and term mode (csg32, csg256 balanced),
     and the 600-sphere chain whose tree is as deep as the depth bound allows (its 16-bit
     stack holds 3 entries per level); every image the oracle's bit for bit.  The same
     scenes of single spheres through the uniform grid (WOLOLO_LANES_GRID=1, build_grid:
-    a DDA walk), and a cluster of overlapping glass spheres (rays that start inside)."""
+    a DDA walk), and a cluster of overlapping glass spheres (rays that start inside).
+    The resumable walk (WOLOLO_LANES_DYN=1: a wave's walking lanes bail out once few
+    lanes walk, the others shade and fetch new rays) on the binary forms: generic
+    primitives, single spheres, term mode, the deep chain and the glass cluster."""
     monkeypatch.setenv(knob, "1")
     monkeypatch.setenv("WOLOLO_LANES_MIN_PRIMS", "64")
     if scene == "union90":
@@ -534,16 +541,25 @@ def test_lanes_wide_bvh_bitexact(knob, scene, monkeypatch):
     info = r.lanes_info()
     if knob == "WOLOLO_LANES_WIDE":
         assert info["depth"] % 3 == 0 and info["depth"] <= 3 * 24, info  # 3 stack entries per 4-wide level
+    if knob == "WOLOLO_LANES_DYN":
+        assert 11 <= info["kind"] <= 13, info  # PathKind kLanesDynSpheres / kLanesDyn / kLanesDynTerms
     r.close()
 
 
 def test_auto_tracer_choices():
     """AUTO: the RTIOW cover (union-only, 487 primitives) takes the lane tracer; csg32 and a
-    128-primitive union-only scene the JIT."""
-    for name, want in [("rtiow_cover", "lanes"), ("csg32", "jit"), ("csg256_balanced_union", "jit")]:
+    128-primitive union-only scene the JIT; csg512_balanced (427 primitives, a union of
+    small terms) the lane tracer's resumable term-mode walk."""
+    for name, want in [("rtiow_cover", "lanes"), ("csg32", "jit"), ("csg256_balanced_union", "jit"),
+                       ("csg512_balanced", "lanes")]:
         r, info = _scene(name, "auto")
         r.render(info.params(width=32, height=18, spp=1))
         assert r.trace_path() == want, (name, r.trace_path())
+        if name == "rtiow_cover":
+            assert r.lanes_info()["kind"] == 3, r.lanes_info()  # kLanesBvhSpheres: the binary walk
+        if name == "csg512_balanced":
+            # > 256 terms: the resumable binary walk in term mode (kLanesDynTerms)
+            assert r.lanes_info()["kind"] == 13, r.lanes_info()
         r.close()
 
 
