@@ -327,6 +327,9 @@ constexpr uint32_t kLaneDepthMax = 24;
 #define WO_LANES_WIDE_DEFAULT 0
 #endif
 constexpr bool kLanesWideDefault = WO_LANES_WIDE_DEFAULT != 0;  // WOLOLO_LANES_WIDE overrides
+#ifndef WO_LANES_TERM2
+#define WO_LANES_TERM2 1  // term visits of two spheres in all: two sphere tests (visit_leaf)
+#endif
 #ifndef WO_LANES_DYN_DEFAULT
 #define WO_LANES_DYN_DEFAULT 0
 #endif
@@ -541,32 +544,63 @@ struct LaneTracer {
             const uint32_t kinds = __float_as_uint(hd.z);
             uint64_t kin[2], kout[2];
             bool valid[2], pos[2];
-#pragma unroll
-            for (int x = 0; x < 2; ++x) {
+            const bool one = tl.y == kNoLit;
+            auto lit_keys = [&](int x, const Ivl& iv) {
                 const uint32_t lit = x == 0 ? tl.x : tl.y;
-                pos[x] = !(lit & kLitNeg);
                 const uint32_t ord = lit & ~kLitNeg;
-                // an inline literal (one or two sphere members; a single sphere repeats
-                // itself as member 1, which leaves the interval and its members as
-                // they are, and a missing second literal is a dummy sphere masked out
-                // below) is branch-free: lanes at different terms stay converged
-                Ivl iv;
-                if ((kinds >> (2 * x)) & 3u) {
-                    WO_WK_N(WO_WORK_SPHERE_TESTS, ((kinds >> (2 * x)) & 3u) == kTermLitSphere ? 1u : 2u);
-                    const float4 g0 = rec[1 + 2 * x], g1 = rec[2 + 2 * x];
-                    float la, lb;
-                    sphere_interval(g0.x, g0.y, g0.z, g0.w, o, d, la, lb);
-                    ivl_first(iv, la, lb);
-                    sphere_interval(g1.x, g1.y, g1.z, g1.w, o, d, la, lb);
-                    ivl_meet(iv, la, lb, 1u);
-                } else {
-                    iv = prim_ivl(ord, o, d, inv, have_inv);
-                }
-                valid[x] = !(iv.a > iv.b) & (iv.b > tmin) & !(x == 1 && lit == kNoLit);
+                pos[x] = !(lit & kLitNeg);
+                valid[x] = !(iv.a > iv.b) & (iv.b > tmin) & !(x == 1 && one);
                 kin[x] = iv.a > tmin ? event_key(iv.a, ord, 0u, iv.ma) : 0ull;
                 kout[x] = iv.b < kInf ? event_key(iv.b, ord, 1u, iv.mb) : kEmptyKey;
+            };
+            // Two spheres in all (WO_LANES_TERM2): one literal of one or two sphere
+            // members, or two literals of one sphere each (csg512's unions, differences
+            // and intersections of pairs) -- two sphere tests instead of the four of the
+            // record's general form, the same intervals and members (a single sphere's
+            // repeated member is a no-op meet), when every lane of the wave has such a term
+            const uint32_t k0 = kinds & 3u, k1 = (kinds >> 2) & 3u;
+            const bool two = (k0 != 0u) & (one | ((k0 == kTermLitSphere) & (k1 == kTermLitSphere)));
+            if (WO_LANES_TERM2 && __ballot(!two) == 0ull) {
+                const bool two0 = k0 == kTermLitSphere2;  // literal 0's second member is the second sphere
+                WO_WK_N(WO_WORK_SPHERE_TESTS, (two0 | !one) ? 2u : 1u);
+                const float4 g0 = rec[1], g1 = rec[two0 ? 2 : 3];
+                float la0, lb0, la1 = kInf, lb1 = -kInf;
+                sphere_interval(g0.x, g0.y, g0.z, g0.w, o, d, la0, lb0);
+                if (__ballot(two0 | !one) != 0ull) {
+                    asm volatile("");
+                    sphere_interval(g1.x, g1.y, g1.z, g1.w, o, d, la1, lb1);
+                }
+                Ivl i0, m0, i1;
+                ivl_first(i0, la0, lb0);
+                m0 = i0;
+                ivl_meet(m0, la1, lb1, 1u);
+                ivl_first(i1, la1, lb1);
+                lit_keys(0, two0 ? m0 : i0);
+                lit_keys(1, i1);
+            } else {
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {
+                    const uint32_t lit = x == 0 ? tl.x : tl.y;
+                    const uint32_t ord = lit & ~kLitNeg;
+                    // an inline literal (one or two sphere members; a single sphere repeats
+                    // itself as member 1, which leaves the interval and its members as
+                    // they are, and a missing second literal is a dummy sphere masked out
+                    // below) is branch-free: lanes at different terms stay converged
+                    Ivl iv;
+                    if ((kinds >> (2 * x)) & 3u) {
+                        WO_WK_N(WO_WORK_SPHERE_TESTS, ((kinds >> (2 * x)) & 3u) == kTermLitSphere ? 1u : 2u);
+                        const float4 g0 = rec[1 + 2 * x], g1 = rec[2 + 2 * x];
+                        float la, lb;
+                        sphere_interval(g0.x, g0.y, g0.z, g0.w, o, d, la, lb);
+                        ivl_first(iv, la, lb);
+                        sphere_interval(g1.x, g1.y, g1.z, g1.w, o, d, la, lb);
+                        ivl_meet(iv, la, lb, 1u);
+                    } else {
+                        iv = prim_ivl(ord, o, d, inv, have_inv);
+                    }
+                    lit_keys(x, iv);
+                }
             }
-            const bool one = tl.y == kNoLit;
             // the literal's value just around key e of the other literal (keys are distinct)
             auto lit_at = [&](int x, uint64_t e) {
                 const bool in = valid[x] & (kin[x] < e) & (e < kout[x]);
