@@ -364,13 +364,13 @@ __device__ __forceinline__ float box_near(float4 lo, float4 hi, F3 ri, F3 oi, fl
 // conjunctions (extract_terms: the leaves and the always list hold terms);
 // 7 / 8 / 9 = 3 / 2 / 6 over a 4-wide tree (lb_collapse4: four child boxes per
 // node, half the dependent node loads of a walk), always with 16-bit stacks.
-// 11 / 12 / 13 = 3 / 2 / 6 with the resumable walk (trace_step, dynamic ray fetch).
+// 11 / 12 / 13 / 14 = 3 / 2 / 6 / 9 with the resumable walk (trace_step, dynamic ray fetch).
 template <int kModeT, bool kCountT>
 struct LaneTracer {
     static constexpr bool kCount = kCountT;
     static constexpr bool kDyn = kModeT >= 11;
     static constexpr bool kResumable = kDyn;
-    static constexpr int kMode = kModeT == 11 ? 3 : kModeT == 12 ? 2 : kModeT == 13 ? 6 : kModeT;
+    static constexpr int kMode = kModeT == 11 ? 3 : kModeT == 12 ? 2 : kModeT == 13 ? 6 : kModeT == 14 ? 9 : kModeT;
     static constexpr bool kBvh = kMode >= 2;
     static constexpr bool kWide = kMode >= 7 && kMode <= 9;
     static constexpr bool kGrid = kMode == 10;
@@ -1066,7 +1066,7 @@ template <int kMode, bool kCount>
 #ifndef WO_LANES_DYN_TERMS_MIN_WAVES
 #define WO_LANES_DYN_TERMS_MIN_WAVES 6  // csg512_balanced: 56.4 ms at 6 (no spill), 57.2 at 7 (31 VGPRs spilled)
 #endif
-__global__ __launch_bounds__(kBlock, kMode == 13 ? WO_LANES_DYN_TERMS_MIN_WAVES
+__global__ __launch_bounds__(kBlock, (kMode == 13 || kMode == 14) ? WO_LANES_DYN_TERMS_MIN_WAVES
                                     : kMode >= 11 ? WO_LANES_DYN_MIN_WAVES
                                     : (kMode == 6 || kMode == 9) ? WO_LANES_TERMS_MIN_WAVES
                                     : (kMode == 2 || kMode == 4 || kMode == 7 || kMode == 8) ? WO_LANES_BVH_MIN_WAVES
@@ -2242,12 +2242,12 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
         LbBox root_box;
         dev->lb_root = lb_build(prims, 0u, (uint32_t)prims.size(), levels, nodes, root_box, dev->lb_depth);
         // 4-wide nodes (WOLOLO_LANES_WIDE=1): refs must fit the 16-bit stack entries.
-        // Off by default: csg512_balanced 82.0 -> 70.5 ms over the binary walk, but the
-        // binary resumable walk (kLanesDynTerms, the default there) takes 56.4; neutral
-        // on csg256 balanced's 65 terms, 16.4 / 16.5 ms; slower on csg32's 14, 8.9 ->
-        // 9.6, and on the RTIOW cover's spheres, 11.7 -> 13.7
+        // Default for term mode over 256 terms (csg512_balanced, resumable walks: 50.1 ->
+        // 44.7 ms over the binary tree; non-resumable 82.0 -> 70.5); neutral on csg256
+        // balanced's 65 terms, 16.4 / 16.5 ms; slower on csg32's 14, 8.9 -> 9.6, and on
+        // the RTIOW cover's spheres, 11.7 -> 13.7
         const char* wv = getenv("WOLOLO_LANES_WIDE");
-        const bool want_wide = wv && *wv ? wv[0] == '1' : kLanesWideDefault;
+        const bool want_wide = wv && *wv ? wv[0] == '1' : (kLanesWideDefault || terms.size() > 256u);
         const uint32_t nrefs = terms.empty() ? n_prims : (uint32_t)terms.size();
         if (want_wide && !(dev->lb_root & kLeafRef) && nrefs < 0x8000u) {
             std::vector<float4> n4;
@@ -2797,7 +2797,7 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
 
 enum PathKind { kLanesLds, kLanesGlobal, kLanesBvh, kLanesBvhSpheres, kLanesBvh16, kLanesBvhSpheres16, kLanesTerms,
                 kLanesWideSpheres, kLanesWide, kLanesWideTerms, kLanesGrid, kLanesDynSpheres, kLanesDyn, kLanesDynTerms,
-                kJit, kInterpLds, kInterpGlobal };
+                kLanesDynWideTerms, kJit, kInterpLds, kInterpGlobal };
 
 template <bool kCount>
 static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
@@ -2830,6 +2830,8 @@ static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<12, kCount>, kBlock, dyn_lds);
     case kLanesDynTerms:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<13, kCount>, kBlock, dyn_lds);
+    case kLanesDynWideTerms:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<14, kCount>, kBlock, dyn_lds);
     case kInterpLds:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_kernel<true, kCount>, kBlock, dyn_lds);
     default:
@@ -2909,6 +2911,11 @@ static void static_launch(PathKind kind, dim3 grid, size_t dyn_lds, hipStream_t 
         break;
     case kLanesDynTerms:
         hipLaunchKernelGGL((pathtrace_lanes_kernel<13, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesDynWideTerms:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<14, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
                            dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
                            lane_bvh(dev));
         break;
@@ -2998,16 +3005,17 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
                     kind = dev->lb_terms   ? kLanesTerms
                            : dev->lb_stack16 ? (dev->lb_spheres_only ? kLanesBvhSpheres16 : kLanesBvh16)
                                              : (dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh);
-                // the resumable walk (dynamic ray fetch) for the binary 32-bit-stack forms:
-                // WOLOLO_LANES_DYN=1 (or 0) over the default, which is term mode over more
-                // than 256 terms (csg512_balanced 84.3 -> 56.4 ms; slower where walks are
-                // short or alike: the RTIOW cover 11.7 -> 12.9-15.5 ms, csg256 balanced's
-                // 65 terms 16.5 -> 18.2)
+                // the resumable walk (dynamic ray fetch) for the binary 32-bit-stack forms
+                // and 4-wide term mode: WOLOLO_LANES_DYN=1 (or 0) over the default, which is
+                // term mode over more than 256 terms (csg512_balanced 84.3 -> 56.4 ms; slower
+                // where walks are short or alike: the RTIOW cover 11.7 -> 12.9-15.5 ms,
+                // csg256 balanced's 65 terms 16.5 -> 18.2)
                 const char* dv = getenv("WOLOLO_LANES_DYN");
                 const bool dyn = dv && *dv ? dv[0] == '1' : (kLanesDynDefault || dev->lb_terms > 256u);
                 if (dyn && kind == kLanesBvhSpheres) kind = kLanesDynSpheres;
                 else if (dyn && kind == kLanesBvh) kind = kLanesDyn;
                 else if (dyn && kind == kLanesTerms) kind = kLanesDynTerms;
+                else if (dyn && kind == kLanesWideTerms) kind = kLanesDynWideTerms;
                 const size_t stacks = ((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u) + 15u) & ~(size_t)15u;
                 dyn_lds = dev->lb_grid ? 0u : stacks + (size_t)dev->lb_top * (dev->lb_wide ? 7u : 4u) * sizeof(float4);
             } else {

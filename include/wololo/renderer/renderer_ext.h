@@ -240,8 +240,8 @@ int wo_renderer_jit_info(Wo_Renderer* r, double* seconds);
 /* The lane tracer's BVH (union-only scenes): out[0] internal nodes, out[1] its
  * depth in internal levels (= the per-lane LDS stack entries; at most 24),
  * out[2] top nodes staged in LDS, out[3] primitives tested on every query (no
- * box), out[4] the kernel form of the last path launch (0-13 the lane tracer's
- * forms, 11-13 the resumable walk; trace_kernels.hip PathKind).  `out` holds 5
+ * box), out[4] the kernel form of the last path launch (0-14 the lane tracer's
+ * forms, 11-14 the resumable walk; trace_kernels.hip PathKind).  `out` holds 5
  * entries.  Returns 0, or -1 when the renderer does not run the lane tracer. */
 int wo_renderer_lanes_info(Wo_Renderer* r, uint32_t* out);
 void wo_free(void* p);

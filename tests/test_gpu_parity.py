@@ -492,9 +492,12 @@ def test_lanes_wide_bvh_bitexact(knob, scene, monkeypatch):
     scenes of single spheres through the uniform grid (WOLOLO_LANES_GRID=1, build_grid:
     a DDA walk), and a cluster of overlapping glass spheres (rays that start inside).
     The resumable walk (WOLOLO_LANES_DYN=1: a wave's walking lanes bail out once few
-    lanes walk, the others shade and fetch new rays) on the binary forms: generic
-    primitives, single spheres, term mode, the deep chain and the glass cluster."""
+    lanes walk, the others shade and fetch new rays) on the binary forms (generic
+    primitives, single spheres, term mode, the deep chain and the glass cluster) and on
+    4-wide term mode."""
     monkeypatch.setenv(knob, "1")
+    if knob == "WOLOLO_LANES_DYN" and scene == "csg256_balanced":
+        monkeypatch.setenv("WOLOLO_LANES_WIDE", "1")  # term mode's resumable 4-wide walk (kind 14)
     monkeypatch.setenv("WOLOLO_LANES_MIN_PRIMS", "64")
     if scene == "union90":
         r = _union_scene()
@@ -542,14 +545,15 @@ def test_lanes_wide_bvh_bitexact(knob, scene, monkeypatch):
     if knob == "WOLOLO_LANES_WIDE":
         assert info["depth"] % 3 == 0 and info["depth"] <= 3 * 24, info  # 3 stack entries per 4-wide level
     if knob == "WOLOLO_LANES_DYN":
-        assert 11 <= info["kind"] <= 13, info  # PathKind kLanesDynSpheres / kLanesDyn / kLanesDynTerms
+        # PathKind kLanesDynSpheres / kLanesDyn / kLanesDynTerms / kLanesDynWideTerms
+        assert info["kind"] == {"csg32": 13, "csg256_balanced": 14, "union90": 12}.get(scene, 11), info
     r.close()
 
 
 def test_auto_tracer_choices():
     """AUTO: the RTIOW cover (union-only, 487 primitives) takes the lane tracer; csg32 and a
     128-primitive union-only scene the JIT; csg512_balanced (427 primitives, a union of
-    small terms) the lane tracer's resumable term-mode walk."""
+    small terms) the lane tracer's resumable 4-wide term-mode walk."""
     for name, want in [("rtiow_cover", "lanes"), ("csg32", "jit"), ("csg256_balanced_union", "jit"),
                        ("csg512_balanced", "lanes")]:
         r, info = _scene(name, "auto")
@@ -558,8 +562,8 @@ def test_auto_tracer_choices():
         if name == "rtiow_cover":
             assert r.lanes_info()["kind"] == 3, r.lanes_info()  # kLanesBvhSpheres: the binary walk
         if name == "csg512_balanced":
-            # > 256 terms: the resumable binary walk in term mode (kLanesDynTerms)
-            assert r.lanes_info()["kind"] == 13, r.lanes_info()
+            # > 256 terms: the resumable 4-wide walk in term mode (kLanesDynWideTerms)
+            assert r.lanes_info()["kind"] == 14, r.lanes_info()
         r.close()
 
 
