@@ -118,6 +118,8 @@ typedef struct Gen {
     int dist_cull;         /* term mode, first pass: skip a group whose sphere begins beyond every lane's best transition */
     int key_vmov;          /* term mode: event-key constants by v_mov (VGPRs) instead of s_mov */
     int term_dist;         /* term mode: a lone sphere / a pair's second literal skipped by lanes whose best precedes it */
+    int cull_barrier;      /* cull[] through an opaque move: 1 in re-collects and sweep steps, 2 re-collects only (WOLOLO_JIT_CULL_BARRIER) */
+    uint32_t ncw;          /* words of cull[] */
     struct SPrim* sprims;  /* the bounded primitives it groups */
     uint32_t nsprims;
     struct SPrim* tunb;    /* term mode: terms without a bounding sphere (tested first, ungrouped) */
@@ -594,8 +596,27 @@ static void gen_collect_terms(Gen* g, int indent) {
     free(p);
 }
 
+/* The cull words through an opaque move: the wave's cull bits are loop-invariant
+ * in the sweep, and without it the compiler turns every bit the re-collect and
+ * the root evaluation test into a 64-bit lane mask ahead of the sweep loop and
+ * keeps them all live -- under SGPR pressure spilled to VGPR lanes (two
+ * v_writelane per bit on every trace, csg256 chain: 60 per trace).  After the
+ * move each test is an s_bitcmp where it is used.  The words are wave-uniform
+ * (every active lane ran the same ballots), but a value carried through the
+ * divergent sweep loop is not provably so: the first lane's copy (exact) puts it
+ * in an SGPR for the move. */
+static void gen_cull_barrier(Gen* g, int indent) {
+    if (!g->cull_barrier) return;
+    for (uint32_t w = 0; w < g->ncw; ++w)
+        bput(g->b,
+             "%*s{ uint32_t cw = (uint32_t)__builtin_amdgcn_readfirstlane((int)cull[%u]); "
+             "asm volatile(\"\" : \"+s\"(cw)); cull[%u] = cw; }\n",
+             indent, "", w, w);
+}
+
 /* the collect of the whole program (either pass) */
 static void gen_collect_all(Gen* g, int indent) {
+    if (!g->first_pass) gen_cull_barrier(g, indent);
     g->nbound = 0;
     if (g->term_mode)
         gen_collect_terms(g, indent);
@@ -1579,6 +1600,13 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         if (v && *v) g.spatial_leaf = (uint32_t)strtoul(v, NULL, 10);
         v = getenv("WOLOLO_JIT_TERM_DIST");
         g.term_dist = v && *v ? v[0] != '0' : 0;
+        v = getenv("WOLOLO_JIT_CULL_BARRIER");
+        /* default 2, re-collects only (1080p64: csg256 chain 13.51 -> 13.21 ms, balanced
+         * 9.70 -> 9.47, csg32 3.273 -> 3.238; the sweep step's barrier as well, 1: 13.29 /
+         * 9.50 / 3.238), except for a general root evaluation over the LDS event list
+         * (csg32_nested 10.92 -> 11.75: its SGPR spills became 564 spilled VGPRs);
+         * the LDS-list case is settled below, where the root's form is known */
+        g.cull_barrier = v && *v ? (int)strtol(v, NULL, 10) : -1;
         v = getenv("WOLOLO_JIT_KEY_VMOV");
         g.key_vmov = v && *v ? v[0] != '0' : 0;
         v = getenv("WOLOLO_JIT_DIST_CULL");
@@ -1823,6 +1851,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * terms (csg32, csg256 balanced) rarely fills the list, and there the eviction
      * code costs csg32 3.608 -> 3.701 ms: off for the union count. */
     if (g.lds_events && n_uterms) bput(&b, "#ifndef WO_LDS_KEEP_SMALLEST\n#define WO_LDS_KEEP_SMALLEST 0\n#endif\n");
+    if (g.cull_barrier < 0) g.cull_barrier = g.lds_events && !n_uterms && !g.term_mode ? 0 : 2;
     /* the register window for deep trees holds 5 events (csg256 chain 29.5 ms at 4,
      * 27.6 at 6, 27.5 at 8; with decision lists 19.36 at 4, 18.47 at 5, 18.65 at 6) */
     if (!g.lds_events) bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW 5\n#endif\n");
@@ -1893,6 +1922,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         for (int a = 0; a < 3; ++a)
             if (axes & (1u << a)) bput(&b, "    const float iv%c = wodev::rcp_dir(d.%c);\n", "xyz"[a], "xyz"[a]);
         uint32_t ncw = nbounds ? (nbounds + 31u) / 32u : 1u;
+        g.ncw = ncw;
         if (g.term_mode) {
             bput(&b, "    uint32_t cull[%u];  // bit k: group k culled for this wave\n", ncw);
             for (uint32_t w = 0; w < ncw; ++w) bput(&b, "    cull[%u] = 0u;\n", w);
@@ -1995,6 +2025,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             bput(&b,
                  "    for (;;) {\n"
                  "      uint32_t r;\n");
+            if (g.cull_barrier == 1) gen_cull_barrier(&g, 6);
             bput(&b,
                  "      // WO_EVAL_BEGIN (the root's value from bits[] and cull[]; tests/test_jit.py compiles it on the host)\n"
                  "      {\n");
