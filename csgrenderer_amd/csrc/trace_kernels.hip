@@ -413,7 +413,13 @@ struct LaneTracer {
     const uint32_t* __restrict__ gcells;
     const uint32_t* __restrict__ gitems;
 
-    __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const { return prog[ordpc[h.ord] + 1u + h.member]; }
+    const WoRec* __restrict__ lleaf;     // single-sphere scenes: per ordinal its leaf record (LaneBvh::leaves)
+    __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const {
+        if constexpr (kSpheresOnly && kBvh)
+            return lleaf[h.ord];  // one load (the record of the ordinal's only member)
+        else
+            return prog[ordpc[h.ord] + 1u + h.member];
+    }
 
     // Interval of primitive `ord` (the general walk's arithmetic, bit for bit).
     __device__ __forceinline__ Ivl prim_ivl(uint32_t ord, F3 o, F3 d, F3& inv, bool& have_inv) {
@@ -1041,6 +1047,7 @@ struct LaneBvh {
     const float4* geo;
     const uint32_t* kind;  // per ordinal, then the always list
     const float4* trec;    // term mode: kTermRecF4 float4 per term
+    const WoRec* leaves;   // single-sphere scenes: per ordinal its leaf record
     uint32_t nalways, root, nprims;
     uint32_t depth;        // internal levels of the tree: the lane stack's entries
     uint32_t ntop;         // nodes [0, ntop) staged in LDS after the lane stacks
@@ -1085,6 +1092,7 @@ __global__ __launch_bounds__(kBlock, (kMode == 13 || kMode == 14) ? WO_LANES_DYN
     tr.lgeo = bvh.geo;
     tr.lkind = bvh.kind;
     tr.ltrec = bvh.trec;
+    tr.lleaf = bvh.leaves;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         tr.glo[a] = bvh.glo[a];
@@ -1408,6 +1416,7 @@ struct WoDev {
     uint32_t lb_terms;     // term mode (kMode 6): terms the BVH's leaves and always list refer to
     uint32_t last_kind;    // the PathKind of the last path launch (wo_dev_lanes_info)
     uint32_t lb_term_off;  // their records (kTermRecF4 float4 each) at this u32 offset of d_lbvh
+    uint32_t lb_leaf_off;  // single-sphere scenes: per ordinal its leaf record (WoRec) at this u32 offset, else 0
     uint32_t lb_top;       // nodes staged in LDS per workgroup
     uint32_t lb_depth;     // internal levels of the lane BVH (<= kLaneDepthMax)
     unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
@@ -2317,9 +2326,16 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     words = (words + 3u) & ~(size_t)3u;
     const size_t term_off = f4 * sizeof(float4) + words * sizeof(uint32_t);
     dev->lb_term_off = (uint32_t)(term_off / sizeof(uint32_t));
-    const size_t bytes = term_off + term_recs.size() * sizeof(float4);
+    // single-sphere scenes: each ordinal's leaf record, so a hit's shading reads it
+    // in one load instead of the ordinal -> pc -> record chain (hit_leaf)
+    const size_t leaf_off = term_off + term_recs.size() * sizeof(float4);
+    dev->lb_leaf_off = dev->lb_spheres_only ? (uint32_t)(leaf_off / sizeof(uint32_t)) : 0u;
+    const size_t bytes = leaf_off + (dev->lb_spheres_only ? (size_t)n_prims * sizeof(WoRec) : 0u);
     if (ensure_buffer(&dev->d_lbvh, &dev->lbvh_cap, bytes, err, errlen)) return -1;
     std::vector<char> blob(bytes);
+    if (dev->lb_spheres_only)
+        for (uint32_t ord = 0; ord < n_prims; ++ord)
+            memcpy(blob.data() + leaf_off + (size_t)ord * sizeof(WoRec), &prog[pc_of[ord] + 1u], sizeof(WoRec));
     memcpy(blob.data(), nodes.data(), nodes.size() * sizeof(float4));
     memcpy(blob.data() + nodes.size() * sizeof(float4), geo.data(), n_prims * sizeof(float4));
     memcpy(blob.data() + f4 * sizeof(float4), kind.data(), n_prims * sizeof(uint32_t));
@@ -2359,6 +2375,9 @@ static LaneBvh lane_bvh(const WoDev* dev) {
     b.trec = dev->lb_terms ? reinterpret_cast<const float4*>(reinterpret_cast<const uint32_t*>(dev->d_lbvh) +
                                                             dev->lb_term_off)
                            : nullptr;
+    b.leaves = dev->lb_leaf_off ? reinterpret_cast<const WoRec*>(reinterpret_cast<const uint32_t*>(dev->d_lbvh) +
+                                                                dev->lb_leaf_off)
+                                : nullptr;
     return b;
 }
 
