@@ -413,12 +413,18 @@ struct LaneTracer {
     const uint32_t* __restrict__ gcells;
     const uint32_t* __restrict__ gitems;
 
-    const WoRec* __restrict__ lleaf;     // single-sphere scenes: per ordinal its leaf record (LaneBvh::leaves)
+    // single-sphere scenes: per ordinal its leaf record, then its material (LaneBvh::leaves)
+    const WoRec* __restrict__ lleaf;
+    static constexpr bool kHitMaterial = kSpheresOnly && kBvh;
     __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const {
         if constexpr (kSpheresOnly && kBvh)
-            return lleaf[h.ord];  // one load (the record of the ordinal's only member)
+            return lleaf[2u * h.ord];  // one load (the record of the ordinal's only member)
         else
             return prog[ordpc[h.ord] + 1u + h.member];
+    }
+    // the leaf's material, copied next to its record: loaded beside it, not after it
+    __device__ __forceinline__ WoMaterial hit_material(const Hit& h, const WoMaterial* __restrict__) const {
+        return reinterpret_cast<const WoMaterial*>(lleaf)[2u * h.ord + 1u];
     }
 
     // Interval of primitive `ord` (the general walk's arithmetic, bit for bit).
@@ -2094,7 +2100,8 @@ static int build_grid(WoDev* dev, const std::vector<LbPrim>& prims, char* err, s
 // primitives and outsized ones (box diagonal > 16x the median, e.g. an RTIOW
 // ground sphere, which every ray meets anyway).  WOLOLO_LANES_BVH=0: none (the
 // general walk only).
-static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n_prims, char* err, size_t errlen) {
+static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n_prims, WoMaterial const* mats,
+                      uint32_t n_mats, char* err, size_t errlen) {
     dev->lb_nodes = dev->lb_always = dev->lb_top = dev->lb_depth = 0;
     dev->lb_root = kNoRef;
     dev->lb_nprims = n_prims;
@@ -2326,16 +2333,22 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     words = (words + 3u) & ~(size_t)3u;
     const size_t term_off = f4 * sizeof(float4) + words * sizeof(uint32_t);
     dev->lb_term_off = (uint32_t)(term_off / sizeof(uint32_t));
-    // single-sphere scenes: each ordinal's leaf record, so a hit's shading reads it
-    // in one load instead of the ordinal -> pc -> record chain (hit_leaf)
+    // single-sphere scenes: each ordinal's leaf record and its material (2 x 32 B), so
+    // a hit's shading reads them in two independent loads instead of the ordinal ->
+    // pc -> record -> material chain (hit_leaf, hit_material)
+    static_assert(sizeof(WoRec) == 32 && sizeof(WoMaterial) == 32, "leaf table entries are 2 x 32 bytes");
     const size_t leaf_off = term_off + term_recs.size() * sizeof(float4);
     dev->lb_leaf_off = dev->lb_spheres_only ? (uint32_t)(leaf_off / sizeof(uint32_t)) : 0u;
-    const size_t bytes = leaf_off + (dev->lb_spheres_only ? (size_t)n_prims * sizeof(WoRec) : 0u);
+    const size_t bytes = leaf_off + (dev->lb_spheres_only ? (size_t)n_prims * 2u * sizeof(WoRec) : 0u);
     if (ensure_buffer(&dev->d_lbvh, &dev->lbvh_cap, bytes, err, errlen)) return -1;
     std::vector<char> blob(bytes);
     if (dev->lb_spheres_only)
-        for (uint32_t ord = 0; ord < n_prims; ++ord)
-            memcpy(blob.data() + leaf_off + (size_t)ord * sizeof(WoRec), &prog[pc_of[ord] + 1u], sizeof(WoRec));
+        for (uint32_t ord = 0; ord < n_prims; ++ord) {
+            const WoRec& L = prog[pc_of[ord] + 1u];
+            char* e = blob.data() + leaf_off + (size_t)ord * 2u * sizeof(WoRec);
+            memcpy(e, &L, sizeof(WoRec));
+            if (L.u0 < n_mats) memcpy(e + sizeof(WoRec), &mats[L.u0], sizeof(WoMaterial));
+        }
     memcpy(blob.data(), nodes.data(), nodes.size() * sizeof(float4));
     memcpy(blob.data() + nodes.size() * sizeof(float4), geo.data(), n_prims * sizeof(float4));
     memcpy(blob.data() + f4 * sizeof(float4), kind.data(), n_prims * sizeof(uint32_t));
@@ -2417,7 +2430,7 @@ extern "C" int wo_dev_upload_scene(WoDev* dev, WoRec const* prog, uint32_t n_rec
     dev->n_prims = n_prims;
     dev->n_mats = n_mats;
     if (build_trav(dev, prog, n_recs, n_prims, err, errlen)) return -1;
-    return build_lbvh(dev, prog, n_recs, n_prims, err, errlen);
+    return build_lbvh(dev, prog, n_recs, n_prims, mats, n_mats, err, errlen);
 }
 
 // ---- scene-specialised kernels (hiprtc) ----
