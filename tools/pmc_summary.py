@@ -44,6 +44,9 @@ def main():
     ap.add_argument("--key", default=None)
     ap.add_argument("--save", default=None)
     ap.add_argument("--copy", default=None, help="copy CSVs to profiles/<prefix>_*.csv")
+    ap.add_argument("--timed", type=int, default=None,
+                    help="also average the last N dispatches of the kernel trace (the bench's timed frames: "
+                         "the first launches run at a ramping clock)")
     a = ap.parse_args()
     res = {}
     kfiles, krows = _rows(os.path.join(a.dir, "kstats"), "*kernel_stats.csv")
@@ -52,6 +55,14 @@ def main():
             res["kernel"] = r["Name"]
             res["calls"] = int(r["Calls"])
             res["avg_ms"] = float(r["AverageNs"]) / 1e6
+    tfiles, trows = _rows(os.path.join(a.dir, "kstats"), "*kernel_trace.csv")
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trows
+            if any(k in r["Kernel_Name"] for k in KERNELS)]
+    if durs:
+        res["median_ms"] = sorted(durs)[len(durs) // 2]
+        if a.timed and len(durs) >= a.timed:
+            res["timed_dispatches"] = a.timed
+            res["timed_avg_ms"] = sum(durs[-a.timed:]) / a.timed
     ffiles, f = counters(a.dir, "fetch")
     wfiles, w = counters(a.dir, "write")
     p1files, p1 = counters(a.dir, "pmc1")
@@ -80,7 +91,7 @@ def main():
         print(f"recorded {a.key} = {res['traffic_bytes']} in {a.save}")
     if a.copy:
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-        for tag, files in (("kernel_stats", kfiles), ("pmc_fetch", ffiles), ("pmc_write", wfiles),
+        for tag, files in (("kernel_stats", kfiles), ("kernel_trace", tfiles), ("pmc_fetch", ffiles), ("pmc_write", wfiles),
                            ("pmc_pmc1", p1files), ("pmc_pmc2", p2files)):
             for i, fn in enumerate(files[:1]):
                 shutil.copy(fn, os.path.join(root, "profiles", f"{a.copy}_{tag}.csv"))
