@@ -330,6 +330,10 @@ constexpr bool kLanesWideDefault = WO_LANES_WIDE_DEFAULT != 0;  // WOLOLO_LANES_
 #ifndef WO_LANES_TERM2
 #define WO_LANES_TERM2 1  // term visits of two spheres in all: two sphere tests (visit_leaf)
 #endif
+#ifndef WO_LANES_HALF_DEFAULT
+#define WO_LANES_HALF_DEFAULT 0
+#endif
+constexpr bool kLanesHalfDefault = WO_LANES_HALF_DEFAULT != 0;  // WOLOLO_LANES_HALF overrides
 #ifndef WO_LANES_DYN_DEFAULT
 #define WO_LANES_DYN_DEFAULT 0
 #endif
@@ -356,6 +360,19 @@ __device__ __forceinline__ float box_near(float4 lo, float4 hi, F3 ri, F3 oi, fl
     return n;
 }
 
+// The same over a child box stored as fp16 (lb_half: lo rounded down, hi up, so
+// the box only grows): q.x = lo.x | lo.y << 16, q.y = lo.z | hi.x << 16, q.z =
+// hi.y | hi.z << 16.  The conversions fold into v_fma_mix_f32.
+__device__ __forceinline__ float h16(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (unsigned short)u); }
+__device__ __forceinline__ float box_near_h(uint4 q, F3 ri, F3 oi, float& far_t) {
+    const float ax = __builtin_fmaf(h16(q.x & 0xffffu), ri.x, -oi.x), bx = __builtin_fmaf(h16(q.y >> 16), ri.x, -oi.x);
+    const float ay = __builtin_fmaf(h16(q.x >> 16), ri.y, -oi.y), by = __builtin_fmaf(h16(q.z & 0xffffu), ri.y, -oi.y);
+    const float az = __builtin_fmaf(h16(q.y & 0xffffu), ri.z, -oi.z), bz = __builtin_fmaf(h16(q.z >> 16), ri.z, -oi.z);
+    const float n = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    far_t = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    return n;
+}
+
 // kMode: 0 general walk over the table in LDS, 1 general walk over the table in
 // global memory, 2 ordered BVH, 3 ordered BVH over single-sphere primitives only
 // (no generic-primitive code: fewer registers); 4 / 5 = 2 / 3 with 16-bit stack
@@ -364,20 +381,23 @@ __device__ __forceinline__ float box_near(float4 lo, float4 hi, F3 ri, F3 oi, fl
 // conjunctions (extract_terms: the leaves and the always list hold terms);
 // 7 / 8 / 9 = 3 / 2 / 6 over a 4-wide tree (lb_collapse4: four child boxes per
 // node, half the dependent node loads of a walk), always with 16-bit stacks.
-// 11 / 12 / 13 / 14 = 3 / 2 / 6 / 9 with the resumable walk (trace_step, dynamic ray fetch).
+// 11 / 12 / 13 / 14 = 3 / 2 / 6 / 9 with the resumable walk (trace_step, dynamic ray fetch);
+// 15 = 3 over nodes of fp16 child boxes (half the bytes: twice the nodes in LDS).
 template <int kModeT, bool kCountT>
 struct LaneTracer {
     static constexpr bool kCount = kCountT;
-    static constexpr bool kDyn = kModeT >= 11;
+    static constexpr bool kDyn = kModeT >= 11 && kModeT <= 14;
     static constexpr bool kResumable = kDyn;
-    static constexpr int kMode = kModeT == 11 ? 3 : kModeT == 12 ? 2 : kModeT == 13 ? 6 : kModeT == 14 ? 9 : kModeT;
+    static constexpr bool kHalf = kModeT == 15;  // binary nodes with fp16 child boxes (lb_half)
+    static constexpr int kMode = kModeT == 11 ? 3 : kModeT == 12 ? 2 : kModeT == 13 ? 6 : kModeT == 14 ? 9
+                               : kModeT == 15 ? 3 : kModeT;
     static constexpr bool kBvh = kMode >= 2;
     static constexpr bool kWide = kMode >= 7 && kMode <= 9;
     static constexpr bool kGrid = kMode == 10;
     static constexpr bool kSpheresOnly = kMode == 3 || kMode == 5 || kMode == 7 || kMode == 10;
     static constexpr bool kStack16 = kMode == 4 || kMode == 5 || kWide;
     static constexpr bool kTerms = kMode == 6 || kMode == 9;
-    static constexpr uint32_t kNodeF4 = kWide ? 7u : 4u;  // float4 per node
+    static constexpr uint32_t kNodeF4 = kWide ? 7u : (kHalf ? 2u : 4u);  // float4 per node
     WorkCounts wk;
     uint64_t tmark;  // section timing (counting builds)
     const WoRec* __restrict__ prog;      // full program (generic primitives, hit leaves)
@@ -404,6 +424,13 @@ struct LaneTracer {
 #else
     typedef const float4* LdsNodes;
     typedef const float4* GlobalNodes;
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(3))) uint4* LdsNodesU4;
+    typedef const __attribute__((address_space(1))) uint4* GlobalNodesU4;
+#else
+    typedef const uint4* LdsNodesU4;
+    typedef const uint4* GlobalNodesU4;
 #endif
     LdsNodes ltop;
     uint32_t ntop;
@@ -762,22 +789,43 @@ struct LaneTracer {
             }
         } else {
             WO_WK_N(WO_WORK_BOUND_TESTS, 2u);
-            float4 a0, a1, b0, b1;
-            if (cur < ntop) {  // the top levels: LDS latency instead of a cache round trip
-                const LdsNodes nd = ltop + 4u * cur;
-                a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
-                asm volatile("");  // the branches' tails differ: the loads are not merged into flat loads
+            float na, nb, fa, fb;
+            uint32_t ra, rb;
+            if constexpr (kHalf) {
+                // per child: lo.x | lo.y, lo.z | hi.x, hi.y | hi.z as fp16 pairs, then its ref;
+                // the fp16 operands go into v_fma_mix_f32 unconverted
+                uint4 qa, qb;
+                if (cur < ntop) {
+                    const LdsNodesU4 nd = (LdsNodesU4)ltop + 2u * cur;
+                    qa = nd[0], qb = nd[1];
+                    asm volatile("");
+                } else {
+                    const GlobalNodesU4 nd = (GlobalNodesU4)lnodes + 2u * cur;
+                    qa = nd[0], qb = nd[1];
+                }
+                na = box_near_h(qa, ri, oi, fa);
+                nb = box_near_h(qb, ri, oi, fb);
+                ra = qa.w;
+                rb = qb.w;
             } else {
-                const GlobalNodes nd = (GlobalNodes)lnodes + 4u * cur;
-                a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                float4 a0, a1, b0, b1;
+                if (cur < ntop) {  // the top levels: LDS latency instead of a cache round trip
+                    const LdsNodes nd = ltop + 4u * cur;
+                    a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                    asm volatile("");  // the branches' tails differ: the loads are not merged into flat loads
+                } else {
+                    const GlobalNodes nd = (GlobalNodes)lnodes + 4u * cur;
+                    a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                }
+                na = box_near(a0, a1, ri, oi, fa);
+                nb = box_near(b0, b1, ri, oi, fb);
+                ra = __float_as_uint(a0.w);
+                rb = __float_as_uint(a1.w);
             }
             // useful range: up to the best event so far
             const float tb = s.best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(s.best >> 32));
-            float fa, fb;
-            const float na = box_near(a0, a1, ri, oi, fa), nb = box_near(b0, b1, ri, oi, fb);
             const bool ha = (fa >= fmaxf(na, tlo)) & (na <= tb);
             const bool hb = (fb >= fmaxf(nb, tlo)) & (nb <= tb);
-            const uint32_t ra = __float_as_uint(a0.w), rb = __float_as_uint(a1.w);
             if (ha & hb) {
                 const bool a_first = na <= nb;
                 cur = a_first ? ra : rb;
@@ -1423,6 +1471,7 @@ struct WoDev {
     uint32_t last_kind;    // the PathKind of the last path launch (wo_dev_lanes_info)
     uint32_t lb_term_off;  // their records (kTermRecF4 float4 each) at this u32 offset of d_lbvh
     uint32_t lb_leaf_off;  // single-sphere scenes: per ordinal its leaf record (WoRec) at this u32 offset, else 0
+    bool lb_half;          // binary nodes of fp16 child boxes (2 float4 per node; kind 15)
     uint32_t lb_top;       // nodes staged in LDS per workgroup
     uint32_t lb_depth;     // internal levels of the lane BVH (<= kLaneDepthMax)
     unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
@@ -2100,6 +2149,31 @@ static int build_grid(WoDev* dev, const std::vector<LbPrim>& prims, char* err, s
 // primitives and outsized ones (box diagonal > 16x the median, e.g. an RTIOW
 // ground sphere, which every ray meets anyway).  WOLOLO_LANES_BVH=0: none (the
 // general walk only).
+static uint32_t lb_node_f4(const WoDev* dev) { return dev->lb_wide ? 7u : (dev->lb_half ? 2u : 4u); }
+
+// fp16 bits of x rounded toward +inf (`up`) or -inf (host): the nearest fp16, one
+// step further when it lies on the wrong side of x (an overflow rounds to the
+// infinity on its side, which a box bound may be)
+static uint32_t half_dir(float x, bool up) {
+    const _Float16 h = (_Float16)x;
+    uint16_t b;
+    memcpy(&b, &h, sizeof b);
+    const float back = (float)h;
+    if (up && back < x) {
+        b = b == 0x8000u ? 0x0001u : (b & 0x8000u) ? (uint16_t)(b - 1u) : (b == 0x7c00u ? b : (uint16_t)(b + 1u));
+    } else if (!up && back > x) {
+        b = b == 0x0000u ? 0x8001u : (b & 0x8000u) ? (b == 0xfc00u ? b : (uint16_t)(b + 1u)) : (uint16_t)(b - 1u);
+    }
+    return b;
+}
+static uint32_t half_down(float x) { return half_dir(x, false); }
+static uint32_t half_up(float x) { return half_dir(x, true); }
+static uint32_t f_bits(float x) {
+    uint32_t u;
+    memcpy(&u, &x, sizeof u);
+    return u;
+}
+
 static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n_prims, WoMaterial const* mats,
                       uint32_t n_mats, char* err, size_t errlen) {
     dev->lb_nodes = dev->lb_always = dev->lb_top = dev->lb_depth = 0;
@@ -2308,14 +2382,35 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
             dev->lb_root = 0u;
         }
     }
-    const uint32_t node_f4 = dev->lb_wide ? 7u : 4u;
+    // fp16 child boxes (WOLOLO_LANES_HALF=1; binary single-sphere trees, kind 15): each
+    // node's two children as 6 fp16 (lo rounded down, hi up) + ref = 2 x 16 bytes
+    {
+        const char* hv = getenv("WOLOLO_LANES_HALF");
+        const bool spheres = terms.empty() && std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
+        dev->lb_half = (hv && *hv ? hv[0] == '1' : kLanesHalfDefault) && spheres && !dev->lb_wide && !dev->lb_grid &&
+                       !nodes.empty() && !(dev->lb_root & kLeafRef);
+        if (dev->lb_half) {
+            const size_t nn = nodes.size() / 4u;
+            std::vector<float4> hn(2u * nn);
+            for (size_t i = 0; i < nn; ++i)
+                for (int c = 0; c < 2; ++c) {
+                    const float4 lo = nodes[4u * i + 2u * (uint32_t)c], hi = nodes[4u * i + 2u * (uint32_t)c + 1u];
+                    const uint32_t ref = f_bits(c == 0 ? nodes[4u * i].w : nodes[4u * i + 1u].w);
+                    const uint32_t q[3] = {half_down(lo.x) | half_down(lo.y) << 16, half_down(lo.z) | half_up(hi.x) << 16,
+                                           half_up(hi.y) | half_up(hi.z) << 16};
+                    hn[2u * i + (uint32_t)c] = make_float4(bits_f(q[0]), bits_f(q[1]), bits_f(q[2]), bits_f(ref));
+                }
+            nodes.swap(hn);
+        }
+    }
+    const uint32_t node_f4 = lb_node_f4(dev);
     dev->lb_nodes = (uint32_t)(nodes.size() / node_f4);
     dev->lb_always = (uint32_t)always.size();
     {
         // 16-bit stack entries when every ref fits 15 bits (WOLOLO_LANES_STACK16=1; always for 4-wide nodes)
         const char* s16 = getenv("WOLOLO_LANES_STACK16");
-        dev->lb_stack16 = dev->lb_wide ||
-                          (terms.empty() && dev->lb_nodes < 0x8000u && n_prims < 0x8000u && s16 && s16[0] == '1');
+        dev->lb_stack16 = dev->lb_wide || (!dev->lb_half && terms.empty() && dev->lb_nodes < 0x8000u &&
+                                           n_prims < 0x8000u && s16 && s16[0] == '1');
         // the top nodes fill what the stacks leave of kLanesBvhLds (8 workgroups per CU)
         const size_t stacks =
             ((((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u)) + 15u) & ~(size_t)15u);
@@ -2365,7 +2460,7 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
 
 static LaneBvh lane_bvh(const WoDev* dev) {
     LaneBvh b;
-    const uint32_t node_f4 = dev->lb_wide ? 7u : 4u;
+    const uint32_t node_f4 = lb_node_f4(dev);
     b.nodes = dev->d_lbvh;
     b.geo = dev->d_lbvh + node_f4 * dev->lb_nodes;
     b.kind = reinterpret_cast<const uint32_t*>(dev->d_lbvh + node_f4 * dev->lb_nodes + dev->lb_nprims);
@@ -2829,7 +2924,7 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
 
 enum PathKind { kLanesLds, kLanesGlobal, kLanesBvh, kLanesBvhSpheres, kLanesBvh16, kLanesBvhSpheres16, kLanesTerms,
                 kLanesWideSpheres, kLanesWide, kLanesWideTerms, kLanesGrid, kLanesDynSpheres, kLanesDyn, kLanesDynTerms,
-                kLanesDynWideTerms, kJit, kInterpLds, kInterpGlobal };
+                kLanesDynWideTerms, kLanesBvhSpheresHalf, kJit, kInterpLds, kInterpGlobal };
 
 template <bool kCount>
 static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
@@ -2864,6 +2959,8 @@ static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<13, kCount>, kBlock, dyn_lds);
     case kLanesDynWideTerms:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<14, kCount>, kBlock, dyn_lds);
+    case kLanesBvhSpheresHalf:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<15, kCount>, kBlock, dyn_lds);
     case kInterpLds:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_kernel<true, kCount>, kBlock, dyn_lds);
     default:
@@ -2948,6 +3045,11 @@ static void static_launch(PathKind kind, dim3 grid, size_t dyn_lds, hipStream_t 
         break;
     case kLanesDynWideTerms:
         hipLaunchKernelGGL((pathtrace_lanes_kernel<14, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
+                           lane_bvh(dev));
+        break;
+    case kLanesBvhSpheresHalf:
+        hipLaunchKernelGGL((pathtrace_lanes_kernel<15, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
                            dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
                            lane_bvh(dev));
         break;
@@ -3048,8 +3150,9 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
                 else if (dyn && kind == kLanesBvh) kind = kLanesDyn;
                 else if (dyn && kind == kLanesTerms) kind = kLanesDynTerms;
                 else if (dyn && kind == kLanesWideTerms) kind = kLanesDynWideTerms;
+                if (dev->lb_half && kind == kLanesBvhSpheres) kind = kLanesBvhSpheresHalf;
                 const size_t stacks = ((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u) + 15u) & ~(size_t)15u;
-                dyn_lds = dev->lb_grid ? 0u : stacks + (size_t)dev->lb_top * (dev->lb_wide ? 7u : 4u) * sizeof(float4);
+                dyn_lds = dev->lb_grid ? 0u : stacks + (size_t)dev->lb_top * lb_node_f4(dev) * sizeof(float4);
             } else {
                 kind = table <= kLanesLdsBudget ? kLanesLds : kLanesGlobal;
                 dyn_lds = kind == kLanesLds ? table : 0u;

@@ -483,7 +483,8 @@ def test_lanes_bvh_depth_bound(levels, monkeypatch):
                                         ["union90", "rtiow_cover", "csg32", "csg256_balanced", "deep600"]] +
                          [("WOLOLO_LANES_GRID", s) for s in ["rtiow_cover", "deep600", "glass200"]] +
                          [("WOLOLO_LANES_DYN", s) for s in
-                          ["union90", "rtiow_cover", "csg32", "csg256_balanced", "deep600", "glass200"]])
+                          ["union90", "rtiow_cover", "csg32", "csg256_balanced", "deep600", "glass200"]] +
+                         [("WOLOLO_LANES_HALF", s) for s in ["rtiow_cover", "deep600", "glass200", "rtiow16"]])
 def test_lanes_wide_bvh_bitexact(knob, scene, monkeypatch):
     """4-wide lane BVH (WOLOLO_LANES_WIDE=1, lb_collapse4): spheres-only (rtiow), generic
     primitives (boxes, half-spaces: the union scene) and term mode (csg32, csg256 balanced),
@@ -494,8 +495,12 @@ def test_lanes_wide_bvh_bitexact(knob, scene, monkeypatch):
     The resumable walk (WOLOLO_LANES_DYN=1: a wave's walking lanes bail out once few
     lanes walk, the others shade and fetch new rays) on the binary forms (generic
     primitives, single spheres, term mode, the deep chain and the glass cluster) and on
-    4-wide term mode."""
+    4-wide term mode.  Binary single-sphere trees with fp16 child boxes (WOLOLO_LANES_HALF=1:
+    lo rounded down and hi up, so a box only grows and the culling stays conservative)."""
     monkeypatch.setenv(knob, "1")
+    if scene == "rtiow16":  # fp16 nodes asked for together with 16-bit stacks: the fp16 form (its 32-bit stack)
+        monkeypatch.setenv("WOLOLO_LANES_STACK16", "1")
+        scene = "rtiow_cover"
     if knob == "WOLOLO_LANES_DYN" and scene == "csg256_balanced":
         monkeypatch.setenv("WOLOLO_LANES_WIDE", "1")  # term mode's resumable 4-wide walk (kind 14)
     monkeypatch.setenv("WOLOLO_LANES_MIN_PRIMS", "64")
@@ -544,6 +549,8 @@ def test_lanes_wide_bvh_bitexact(knob, scene, monkeypatch):
     info = r.lanes_info()
     if knob == "WOLOLO_LANES_WIDE":
         assert info["depth"] % 3 == 0 and info["depth"] <= 3 * 24, info  # 3 stack entries per 4-wide level
+    if knob == "WOLOLO_LANES_HALF":
+        assert info["kind"] == 15, info  # PathKind kLanesBvhSpheresHalf: fp16 child boxes
     if knob == "WOLOLO_LANES_DYN":
         # PathKind kLanesDynSpheres / kLanesDyn / kLanesDynTerms / kLanesDynWideTerms
         assert info["kind"] == {"csg32": 13, "csg256_balanced": 14, "union90": 12}.get(scene, 11), info
