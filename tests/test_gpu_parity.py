@@ -608,6 +608,8 @@ def test_jit_event_windows(window, monkeypatch):
     {"WOLOLO_JIT_TERMS": "0"},  # the event-list form on csg32
     {"WOLOLO_JIT_TERMS": "1", "WOLOLO_JIT_DIST_CULL": "1"},  # groups beyond every lane's best skipped
     {"WOLOLO_JIT_TERMS": "1", "WOLOLO_JIT_TERM_DIST": "1", "WOLOLO_JIT_KEY_VMOV": "1"},  # terms beyond a lane's best
+    {"WOLOLO_JIT_CULL_BARRIER": "1"},  # cull words through the opaque move in sweep steps too (nested: LDS list)
+    {"WOLOLO_JIT_CULL_BARRIER": "0"},  # no opaque move (the hoisted masks)
 ])
 def test_jit_culling_knobs(knobs, monkeypatch):
     """The wave-level member skip, the bound-around-a-lone-primitive rule, the
