@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--no-encode", action="store_true")
+    ap.add_argument("--tile-rows", type=int, default=4, help="rows per row-cyclic band (bench.py --tile-rows)")
     args = ap.parse_args()
 
     import torch
@@ -54,7 +55,7 @@ def main():
     info = scenes.build(args.scene, r)
     over = {k: getattr(args, k) for k in ("width", "height", "spp") if getattr(args, k)}
     p = info.params(**over)
-    W, H, T, F = p.width, p.height, 4, args.frames
+    W, H, T, F = p.width, p.height, args.tile_rows, args.frames
     main_s = torch.cuda.current_stream()
 
     def timed(fn):
