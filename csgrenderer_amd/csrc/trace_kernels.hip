@@ -330,6 +330,9 @@ constexpr bool kLanesWideDefault = WO_LANES_WIDE_DEFAULT != 0;  // WOLOLO_LANES_
 #ifndef WO_LANES_TERM2
 #define WO_LANES_TERM2 1  // term visits of two spheres in all: two sphere tests (visit_leaf)
 #endif
+#ifndef WO_LANES_PRIO
+#define WO_LANES_PRIO 0  // wave priority while a binary walk trip issues its node load (0: unchanged)
+#endif
 #ifndef WO_LANES_HALF_DEFAULT
 #define WO_LANES_HALF_DEFAULT 0
 #endif
@@ -809,6 +812,9 @@ struct LaneTracer {
                 rb = qb.w;
             } else {
                 float4 a0, a1, b0, b1;
+#if WO_LANES_PRIO
+                __builtin_amdgcn_s_setprio(WO_LANES_PRIO);  // a wave about to issue its node load goes first
+#endif
                 if (cur < ntop) {  // the top levels: LDS latency instead of a cache round trip
                     const LdsNodes nd = ltop + 4u * cur;
                     a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
@@ -817,6 +823,9 @@ struct LaneTracer {
                     const GlobalNodes nd = (GlobalNodes)lnodes + 4u * cur;
                     a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
                 }
+#if WO_LANES_PRIO
+                __builtin_amdgcn_s_setprio(0);
+#endif
                 na = box_near(a0, a1, ri, oi, fa);
                 nb = box_near(b0, b1, ri, oi, fb);
                 ra = __float_as_uint(a0.w);
