@@ -333,6 +333,9 @@ constexpr bool kLanesWideDefault = WO_LANES_WIDE_DEFAULT != 0;  // WOLOLO_LANES_
 #ifndef WO_LANES_PRIO
 #define WO_LANES_PRIO 1  // wave priority while a walk trip issues its node load (0: unchanged; RTIOW 11.67 -> 11.58 ms)
 #endif
+#ifndef WO_LANES_PRIO_LEAF
+#define WO_LANES_PRIO_LEAF 1  // the same at a sphere leaf's geometry load (single-sphere walks; RTIOW 11.565 -> 11.505 ms)
+#endif
 #ifndef WO_LANES_HALF_DEFAULT
 #define WO_LANES_HALF_DEFAULT 0
 #endif
@@ -675,7 +678,13 @@ struct LaneTracer {
             // count and the events inside the sqrt branch, no empty interval formed
             // (the specialised kernel's lone spheres; same bits as prim_ivl's form)
             WO_WK(WO_WORK_SPHERE_TESTS);
+#if WO_LANES_PRIO_LEAF
+            __builtin_amdgcn_s_setprio(WO_LANES_PRIO_LEAF);
+#endif
             const float4 g = lgeo[ord];
+#if WO_LANES_PRIO_LEAF
+            __builtin_amdgcn_s_setprio(0);
+#endif
             float b, ll;
             sphere_bl(g.x, g.y, g.z, o, d, b, ll);
             const float disc = g.w - ll;
