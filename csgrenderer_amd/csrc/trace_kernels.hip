@@ -34,6 +34,11 @@
 #include <vector>
 
 #include "wo_dev.h"
+// the static kernels raise the wave priority while a hit's leaf and material loads issue
+// (RTIOW cover 11.50 -> 11.47 ms in two pairs; the specialised kernel keeps 0: csg32 3.261 vs 3.266)
+#ifndef WO_SHADE_PRIO
+#define WO_SHADE_PRIO 1
+#endif
 #include "wo_device_common.h"
 #include "wololo/wo_scene.h"
 
