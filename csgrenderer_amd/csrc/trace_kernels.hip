@@ -341,6 +341,9 @@ constexpr bool kLanesWideDefault = WO_LANES_WIDE_DEFAULT != 0;  // WOLOLO_LANES_
 #ifndef WO_LANES_PRIO_LEAF
 #define WO_LANES_PRIO_LEAF 1  // the same at a sphere leaf's geometry load (single-sphere walks; RTIOW 11.565 -> 11.505 ms)
 #endif
+#ifndef WO_LANES_PRIO_TERM
+#define WO_LANES_PRIO_TERM 0  // the same at a term record's load (term mode)
+#endif
 #ifndef WO_LANES_HALF_DEFAULT
 #define WO_LANES_HALF_DEFAULT 0
 #endif
@@ -589,7 +592,13 @@ struct LaneTracer {
         if constexpr (kTerms) {
             // the record's header and both literals' inline spheres: independent loads
             const float4* rec = ltrec + kTermRecF4 * ref;
+#if WO_LANES_PRIO_TERM
+            __builtin_amdgcn_s_setprio(WO_LANES_PRIO_TERM);
+#endif
             const float4 hd = rec[0];
+#if WO_LANES_PRIO_TERM
+            __builtin_amdgcn_s_setprio(0);
+#endif
             const uint2 tl = make_uint2(__float_as_uint(hd.x), __float_as_uint(hd.y));
             const uint32_t kinds = __float_as_uint(hd.z);
             uint64_t kin[2], kout[2];
