@@ -84,6 +84,12 @@ def parse():
                     help="rank 0 checks the assembled frame against a single full-frame render (bit-exact)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-dispatch HBM bytes measured by rocprofv3 --pmc (profiles/*.json) for roofline.traffic")
+    ap.add_argument("--side-scenes", default="csg32_nested",
+                    help="N=1 csg32 runs only: comma-separated scenes measured after the headline in the same "
+                         "invocation and reported as sub-objects of the line ('' = none)")
+    ap.add_argument("--no-draw-frame", action="store_true",
+                    help="N=1: skip the draw_frame leg (wo_renderer_draw_frame frames, map-back included)")
+    ap.add_argument("--draw-frames", type=int, default=60, help="frames of the draw_frame leg")
     return ap.parse_args()
 
 
@@ -304,12 +310,108 @@ def main():
                             "frames_in_flight": args.frames_in_flight, "prewarm_frames": prewarm})
         if verified is not None:
             line["verified_vs_full_render"] = verified
+        if world == 1 and info.mode == wl.MODE_PATHTRACE and not args.no_draw_frame:
+            line["draw_frame"] = draw_frame_leg(r, params, args, line["fps"])
+        if world == 1 and args.scene == "csg32" and args.side_scenes and not (args.width or args.height or args.spp):
+            for name in [x for x in args.side_scenes.split(",") if x]:
+                line[name.replace("csg32_", "")] = side_scene(name, args, dev)
         print(json.dumps(line), flush=True)
     r.close()
     if world > 1:
         dist.destroy_process_group()
     if not verified_all:
         sys.exit(3)
+
+
+def draw_frame_leg(r, params, args, kernel_fps):
+    """The product's frame rate: frames through wo_renderer_draw_frame (renderer.c:2085-2219's
+    replacement), i.e. render + present encode + map-back to pinned host memory, each frame
+    presented.  The pipeline is drained before and after the timed frames, so the time holds
+    exactly `draw_frames` renders and the last frame's map-back.  Stamps of the same frames
+    (HIP events of the pipeline) give the render and map-back times."""
+    r.set_draw_params(params, pin_time=True)
+    for _ in range(3):
+        r.draw_frame()
+    r.finish()
+    n = max(args.draw_frames, 2)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        r.draw_frame()
+    r.finish()
+    dt = time.perf_counter() - t0
+    r.set_frame_stamps(True)
+    for _ in range(min(n, 20)):
+        r.draw_frame()
+    r.finish()
+    st = r.frame_stamps()
+    r.set_frame_stamps(False)
+    fps = n / dt
+    out = {"fps": round(fps, 3), "ms_per_frame": round(dt / n * 1e3, 4), "frames": n,
+           "vs_kernel_fps": round(fps / kernel_fps, 4) if kernel_fps else None,
+           "map_back": "present encode (B8G8R8A8 sRGB) + D2H to pinned host memory on a copy stream; "
+                       "float frame on demand"}
+    if len(st) > 2:
+        import statistics
+        out["stamps"] = {
+            "frames": len(st),
+            "render_ms_median": round(statistics.median(e - b for b, e, _ in st), 4),
+            "map_back_ms_median": round(statistics.median(m - e for _, e, m in st), 4),
+            "render_gap_ms_median": round(statistics.median(st[k + 1][0] - st[k][1] for k in range(len(st) - 1)), 4),
+            "next_render_inside_map_back": sum(1 for k in range(len(st) - 1) if st[k + 1][0] < st[k][2]),
+        }
+    return out
+
+
+def side_scene(name, args, dev):
+    """Another BASELINE scene at the headline's size, timed like the headline (N = 1, same
+    steps, HIP events on the launch stream) in the same invocation: ms_per_step, value and
+    the executed-work roofline."""
+    import torch
+
+    from csgrenderer_amd import scenes
+    from csgrenderer_amd import wololo as wl
+    r = wl.Renderer(f"side-{name}", max_nodes=4096)
+    info = scenes.build(name, r)
+    params = info.params(max_depth=args.depth)
+    r.set_tracer("interpreter" if args.jit == 0 else args.tracer)
+    W, H, T = params.width, params.height, args.tile_rows
+    out = torch.empty((wl.local_rows(H, T, 1), W, 4), dtype=torch.float32, device=dev)
+    seg = torch.zeros(1, dtype=torch.int64, device=dev)
+    cs = torch.cuda.current_stream(dev)
+    k0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    k1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            k0[i].record(cs)
+        r.render_rows_device(params, out.data_ptr(), T, 0, 1, cs.cuda_stream, seg.data_ptr())
+        if i is not None:
+            k1[i].record(cs)
+
+    step()
+    torch.cuda.synchronize()
+    t_pw = time.perf_counter()
+    while time.perf_counter() - t_pw < args.prewarm_s:
+        step()
+        torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    seg.zero_()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    segs = int(seg.item())
+    k_ms = sum(k0[i].elapsed_time(k1[i]) for i in range(args.steps)) / args.steps
+    work = None if args.no_count_work else r.count_work(params, T, 0, 1)
+    sub_args = argparse.Namespace(**vars(args))
+    sub_args.scene, sub_args.no_cpu_baseline = name, True
+    line = report_line(sub_args, r, info, params, 1, elapsed, segs, segs, k_ms, work, {})
+    r.close()
+    return {k: line[k] for k in ("value", "unit", "ms_per_step", "fps", "segments_per_frame", "roofline")} | {
+        "workload": line["config"]["workload"]}
 
 
 def report_line(args, r, info, params, world, elapsed_s, segs_all, segs_local, k_ms, work, cfg_extra):

@@ -87,6 +87,7 @@ Wo_Renderer* wo_renderer_new(Wo_App* app, char const* name, size_t max_node_coun
         if (r->name) memcpy(r->name, name, n + 1);
     }
     r->app = app;
+    r->last_slot = -1;
     /* material 0: default lambertian grey */
     r->mats[0].kind = WO_MAT_LAMBERTIAN;
     r->mats[0].albedo[0] = r->mats[0].albedo[1] = r->mats[0].albedo[2] = 0.5f;
@@ -216,6 +217,9 @@ int wo_renderer_set_devices(Wo_Renderer* r, int n) {
     /* fault injection for the tests: rank k's set-up fails (WOLOLO_FAULT_RANK=k) */
     const char* fk = getenv("WOLOLO_FAULT_RANK");
     const int fault_rank = fk && *fk ? atoi(fk) : -1;
+    /* the root's streams may still read the ranks' buffers (a device frame's
+     * host-staged H2D from a rank's pinned copy): drain them first */
+    if (r->ndevs > 1) (void)wo_dev_sync(r->dev);
     for (uint32_t i = 1; i < r->ndevs; ++i) {
         wo_dev_destroy(r->devs[i]);
         r->devs[i] = NULL;
@@ -264,6 +268,7 @@ void wo_renderer_del(Wo_Renderer* r) {
     if (r->jit_job) (void)wo_jit_job_finish(r->jit_job, NULL, 0);
     jit_old_reap(r, 1);
     free(r->jit_want);
+    if (r->ndevs > 1) (void)wo_dev_sync(r->dev); /* as in set_devices */
     for (uint32_t i = 1; i < r->ndevs; ++i) wo_dev_destroy(r->devs[i]);
     if (r->dev) wo_dev_destroy(r->dev);
     free(r->nodes);
@@ -708,7 +713,11 @@ int wo_assemble_rows_device(void const* d_gathered, void* d_frame, uint32_t widt
  * on the GPU: present.c) as the last frame, and dump it as a binary PPM when
  * WOLOLO_OUTPUT names a file (the headless stand-in for the swapchain,
  * ref renderer.c:2160-2211). */
-static void present(Wo_Renderer* r, float const* px, uint32_t const* bgra8, uint32_t w, uint32_t h) {
+static void present(Wo_Renderer* r, int slot, float const* px, uint32_t const* bgra8, uint32_t w, uint32_t h) {
+    r->last_slot = slot;
+    if (r->stamps && r->n_stamps < sizeof r->stamp_log / sizeof r->stamp_log[0] &&
+        wo_dev_slot_stamps(r->dev, slot, r->stamp_log[r->n_stamps]) == 0)
+        r->n_stamps++;
     r->last_frame = px;
     r->last_bgra8 = bgra8;
     r->last_w = w;
@@ -729,7 +738,7 @@ static int retire_slot(Wo_Renderer* r, int slot) {
         wo_set_error("frame wait failed: %s", err);
         return -1;
     }
-    present(r, px, bgra8, r->pend_w[slot], r->pend_h[slot]);
+    present(r, slot, px, bgra8, r->pend_w[slot], r->pend_h[slot]);
     return 0;
 }
 
@@ -786,7 +795,10 @@ static int submit_frame(Wo_Renderer* r, Wo_RenderParams p, int slot, int accumul
     WoFrame fr;
     if (wo_renderer_frame_desc(r, &p, 4, 0, nr, &fr)) return -1;
     const int cur = r->ndevs > 1 ? wo_dev_current() : -1;
-    int rc = wo_dev_frame_submit_ranks(r->devs, nr, &fr, slot, acc ? d_acc : NULL, total, err, sizeof err);
+    /* the synchronous render hands its float frame back; a presented frame maps
+     * back its present encode, and the float pixels only on request */
+    const int map_float = slot == WO_SLOT_SYNC || r->map_float;
+    int rc = wo_dev_frame_submit_ranks(r->devs, nr, &fr, slot, acc ? d_acc : NULL, total, map_float, err, sizeof err);
     if (cur >= 0) (void)wo_dev_select(cur);
     if (rc) {
         wo_set_error("frame submit failed: %s", err);
@@ -827,7 +839,17 @@ void wo_renderer_set_progressive(Wo_Renderer* r, int on) {
 
 uint32_t wo_renderer_accumulated_spp(Wo_Renderer* r) { return r->acc_valid ? r->acc_spp : 0u; }
 
+/* The presented frame's float pixels are mapped back when asked for: its slot
+ * keeps the device frame until the next draw_frame submits into it. */
 float const* wo_renderer_last_frame(Wo_Renderer* r, uint32_t* width, uint32_t* height) {
+    if (!r->last_frame && r->last_bgra8 && r->dev && r->last_slot >= 0) {
+        char err[256] = {0};
+        float const* px = NULL;
+        if (wo_dev_frame_map_float(r->dev, r->last_slot, &px, err, sizeof err) == 0)
+            r->last_frame = px;
+        else
+            wo_set_error("last frame: %s", err);
+    }
     if (width) *width = r->last_frame ? r->last_w : 0u;
     if (height) *height = r->last_frame ? r->last_h : 0u;
     return r->last_frame;
@@ -837,6 +859,31 @@ uint32_t const* wo_renderer_last_frame_bgra8(Wo_Renderer* r, uint32_t* width, ui
     if (width) *width = r->last_bgra8 ? r->last_w : 0u;
     if (height) *height = r->last_bgra8 ? r->last_h : 0u;
     return r->last_bgra8;
+}
+
+void wo_renderer_set_map_float(Wo_Renderer* r, int every_frame) {
+    if (r) r->map_float = every_frame != 0;
+}
+
+int wo_renderer_set_frame_stamps(Wo_Renderer* r, int on) {
+    if (!r || !r->dev) return -1;
+    if (wo_renderer_finish(r)) return -1;
+    char err[256] = {0};
+    if (wo_dev_set_stamps(r->dev, on, err, sizeof err)) {
+        wo_set_error("%s", err);
+        return -1;
+    }
+    r->stamps = on != 0;
+    r->n_stamps = 0;
+    return 0;
+}
+
+int wo_renderer_frame_stamps(Wo_Renderer* r, double* out, int max_frames) {
+    if (!r || !out || max_frames < 0) return -1;
+    uint32_t n = r->n_stamps < (uint32_t)max_frames ? r->n_stamps : (uint32_t)max_frames;
+    memcpy(out, r->stamp_log, (size_t)n * sizeof r->stamp_log[0]);
+    r->n_stamps = 0;
+    return (int)n;
 }
 
 int wo_srgb8_encode_device(void const* d_rgba, void* d_bgra8, size_t pixels, void* stream) {

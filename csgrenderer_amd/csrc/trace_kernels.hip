@@ -1528,7 +1528,20 @@ struct WoDev {
     size_t dbgra_cap[WO_SLOTS];
     uint32_t* h_bgra[WO_SLOTS];
     size_t hbgra_cap[WO_SLOTS];
-    hipEvent_t slot_ev[WO_SLOTS];
+    hipEvent_t slot_ev[WO_SLOTS];  // the slot's map-back is done (on copy_stream)
+    // Map-back of presented frames: the present encode and
+    // the D2H copies run on their own stream, gated by rend_ev (the slot's frame is
+    // rendered), so the next frame's kernel starts as soon as this one ends.
+    hipStream_t copy_stream;
+    hipEvent_t rend_ev[WO_SLOTS];
+    bool slot_float[WO_SLOTS];  // the float frame was copied with the last map-back
+    size_t slot_pixels[WO_SLOTS];  // pixels of the slot's last frame
+    bool slot_recorded[WO_SLOTS];  // slot_ev has been recorded (never wait on an unrecorded event)
+    // pipeline timestamps (wo_dev_set_stamps): render begin / render end / map-back end
+    bool stamps;
+    hipEvent_t st_base;
+    hipEvent_t st_ev[WO_SLOTS][3];
+    bool st_valid[WO_SLOTS];
     // several devices per renderer (wo_dev_frame_submit_ranks): on the root,
     // the rank-major buffer the ranks' shares are copied into and the event that
     // opens a slot to the ranks; on every rank, its share of the frame and the
@@ -1615,6 +1628,13 @@ extern "C" int wo_dev_create(int device, WoDev** out, char* err, size_t errlen) 
         delete dev;
         return -1;
     }
+    e = hipStreamCreateWithFlags(&dev->copy_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "hipStreamCreate(copy)", e);
+        (void)hipStreamDestroy(dev->stream);
+        delete dev;
+        return -1;
+    }
     *out = dev;
     return 0;
 }
@@ -1646,9 +1666,14 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
         if (dev->gate_ev[i]) (void)hipEventDestroy(dev->gate_ev[i]);
         if (dev->d_part[i]) (void)hipFree(dev->d_part[i]);
         if (dev->part_ev[i]) (void)hipEventDestroy(dev->part_ev[i]);
+        if (dev->rend_ev[i]) (void)hipEventDestroy(dev->rend_ev[i]);
+        for (int k = 0; k < 3; ++k)
+            if (dev->st_ev[i][k]) (void)hipEventDestroy(dev->st_ev[i][k]);
     }
+    if (dev->st_base) (void)hipEventDestroy(dev->st_base);
     if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
     if (dev->count_module) (void)hipModuleUnload(dev->count_module);
+    (void)hipStreamDestroy(dev->copy_stream);
     (void)hipStreamDestroy(dev->stream);
     delete dev;
 }
@@ -3420,39 +3445,66 @@ static int prep_slot(WoDev* dev, int slot, uint32_t width, uint32_t height, uint
     if (ensure_pinned((void**)&dev->h_bgra[slot], &dev->hbgra_cap[slot], pixels * sizeof(uint32_t), err, errlen))
         return -1;
     if (ensure_buffer(&dev->d_bgra[slot], &dev->dbgra_cap[slot], pixels * sizeof(uint32_t), err, errlen)) return -1;
+    if (ensure_event(&dev->rend_ev[slot], err, errlen)) return -1;
     return ensure_event(&dev->slot_ev[slot], err, errlen);
 }
 
-// After the frame is in d_slot: the present encode, both copies to the pinned
-// host buffers and the slot event, asynchronous on the device stream.
-static int present_slot(WoDev* dev, int slot, size_t pixels, char* err, size_t errlen) {
-    hipError_t e;
+// Before a frame is rendered into d_slot: the render stream waits for the
+// slot's previous map-back (it reads d_slot / d_bgra on the copy stream), and
+// the render-begin stamp.
+static int open_slot(WoDev* dev, int slot, char* err, size_t errlen) {
+    hipError_t e = dev->slot_recorded[slot] ? hipStreamWaitEvent(dev->stream, dev->slot_ev[slot], 0) : hipSuccess;
+    if (e == hipSuccess && dev->stamps) e = hipEventRecord(dev->st_ev[slot][0], dev->stream);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "frame slot gate", e);
+        return -1;
+    }
+    return 0;
+}
+
+// After the frame is in d_slot (on the render stream): the map-back on the copy
+// stream -- the present encode, its copy to pinned host memory and, when
+// `map_float`, the float frame's copy -- then the slot event.  The render stream
+// does not wait for any of it: the next frame's kernel starts at once.
+static int present_slot(WoDev* dev, int slot, size_t pixels, bool map_float, char* err, size_t errlen) {
+    hipError_t e = dev->stamps ? hipEventRecord(dev->st_ev[slot][1], dev->stream) : hipSuccess;
+    if (e == hipSuccess) e = hipEventRecord(dev->rend_ev[slot], dev->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(dev->copy_stream, dev->rend_ev[slot], 0);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "map-back gate", e);
+        return -1;
+    }
+    dev->slot_float[slot] = map_float || !pixels;
+    dev->slot_pixels[slot] = pixels;
     if (pixels) {
-        // the float frame (wo_renderer_last_frame) and its present encode
-        // (wo_renderer_last_frame_bgra8)
-        if (wo_dev_srgb8(dev->d_slot[slot], dev->d_bgra[slot], pixels, dev->stream, err, errlen)) return -1;
-        e = hipMemcpyAsync(dev->h_slot[slot], dev->d_slot[slot], pixels * sizeof(float4), hipMemcpyDeviceToHost,
-                           dev->stream);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(dev->h_bgra[slot], dev->d_bgra[slot], pixels * sizeof(uint32_t),
-                               hipMemcpyDeviceToHost, dev->stream);
+        // the present encode (wo_renderer_last_frame_bgra8) and, eagerly or on
+        // demand (wo_dev_frame_map_float), the float frame (wo_renderer_last_frame)
+        if (wo_dev_srgb8(dev->d_slot[slot], dev->d_bgra[slot], pixels, dev->copy_stream, err, errlen)) return -1;
+        e = hipMemcpyAsync(dev->h_bgra[slot], dev->d_bgra[slot], pixels * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           dev->copy_stream);
+        if (e == hipSuccess && map_float)
+            e = hipMemcpyAsync(dev->h_slot[slot], dev->d_slot[slot], pixels * sizeof(float4), hipMemcpyDeviceToHost,
+                               dev->copy_stream);
         if (e != hipSuccess) {
             set_err(err, errlen, "hipMemcpyAsync(frame slot)", e);
             return -1;
         }
     }
-    e = hipEventRecord(dev->slot_ev[slot], dev->stream);
+    e = dev->stamps ? hipEventRecord(dev->st_ev[slot][2], dev->copy_stream) : hipSuccess;
+    if (e == hipSuccess) e = hipEventRecord(dev->slot_ev[slot], dev->copy_stream);
     if (e != hipSuccess) {
         set_err(err, errlen, "hipEventRecord", e);
         return -1;
     }
+    dev->slot_recorded[slot] = true;
+    dev->st_valid[slot] = dev->stamps;
     return 0;
 }
 
 static bool present_slot_ok(int slot) { return slot >= 0 && slot <= WO_SLOT_SYNC; }
 
 extern "C" int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, long long* d_accum,
-                                   uint32_t accum_spp, char* err, size_t errlen) {
+                                   uint32_t accum_spp, int map_float, char* err, size_t errlen) {
     if (!present_slot_ok(slot)) {
         snprintf(err, errlen, "bad frame slot %d", slot);
         return -1;
@@ -3465,10 +3517,79 @@ extern "C" int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, l
     }
     if (prep_slot(dev, slot, fr.width, fr.height, wo_rank_local_rows(fr.height, fr.tile_rows, 1u), err, errlen))
         return -1;
+    if (open_slot(dev, slot, err, errlen)) return -1;
     if (wo_dev_launch_ex(dev, &fr, dev->d_slot[slot], dev->stream, nullptr, d_accum, accum_spp, err, errlen))
         return -1;
     // whole frame, one rank: the local rows are the frame rows
-    return present_slot(dev, slot, (size_t)fr.width * fr.height, err, errlen);
+    return present_slot(dev, slot, (size_t)fr.width * fr.height, map_float != 0, err, errlen);
+}
+
+// The float frame of a presented slot whose map-back left it on the device
+// (lazy map-back): copied now, synchronously.  The slot must have been waited
+// for and not submitted again since.
+extern "C" int wo_dev_frame_map_float(WoDev* dev, int slot, float const** host, char* err, size_t errlen) {
+    if (!present_slot_ok(slot) || !dev->slot_ev[slot] || !dev->d_slot[slot] || !dev->h_slot[slot]) {
+        snprintf(err, errlen, "frame slot %d holds no frame", slot);
+        return -1;
+    }
+    if (!dev->slot_float[slot]) {
+        hipError_t e = hipSetDevice(dev->device);
+        const size_t bytes = dev->slot_pixels[slot] * sizeof(float4);
+        if (e == hipSuccess) e = hipMemcpyAsync(dev->h_slot[slot], dev->d_slot[slot], bytes, hipMemcpyDeviceToHost,
+                                                dev->copy_stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(dev->copy_stream);
+        if (e != hipSuccess) {
+            set_err(err, errlen, "float frame map-back", e);
+            return -1;
+        }
+        dev->slot_float[slot] = true;
+    }
+    *host = dev->h_slot[slot];
+    return 0;
+}
+
+// Pipeline timestamps: while on, every frame submitted to a present slot records
+// three timing events (render begin and end on the render stream, map-back end
+// on the copy stream); wo_dev_slot_stamps reads them, in ms after the moment
+// stamps were turned on.
+extern "C" int wo_dev_set_stamps(WoDev* dev, int on, char* err, size_t errlen) {
+    hipError_t e = hipSetDevice(dev->device);
+    auto mk = [&](hipEvent_t* ev) {
+        if (e == hipSuccess && !*ev) e = hipEventCreate(ev);
+    };
+    if (on) {
+        mk(&dev->st_base);
+        for (int i = 0; i < WO_SLOTS; ++i)
+            for (int k = 0; k < 3; ++k) mk(&dev->st_ev[i][k]);
+        if (e == hipSuccess) e = hipEventRecord(dev->st_base, dev->stream);
+    }
+    if (e != hipSuccess) {
+        set_err(err, errlen, "pipeline stamps", e);
+        return -1;
+    }
+    dev->stamps = on != 0;
+    for (int i = 0; i < WO_SLOTS; ++i) dev->st_valid[i] = false;
+    return 0;
+}
+
+extern "C" int wo_dev_slot_stamps(WoDev* dev, int slot, double out[3]) {
+    if (!present_slot_ok(slot) || !dev->st_valid[slot]) return -1;
+    for (int k = 0; k < 3; ++k) {
+        float ms = 0.0f;
+        if (hipEventSynchronize(dev->st_ev[slot][k]) != hipSuccess ||
+            hipEventElapsedTime(&ms, dev->st_base, dev->st_ev[slot][k]) != hipSuccess)
+            return -1;
+        out[k] = ms;
+    }
+    dev->st_valid[slot] = false;
+    return 0;
+}
+
+// The caller's view of the device: every stream of it drained (set_devices /
+// del before releasing ranks whose buffers the root's streams may still read).
+extern "C" int wo_dev_sync(WoDev* dev) {
+    if (!dev) return 0;
+    return hipSetDevice(dev->device) == hipSuccess && hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
 extern "C" int wo_dev_peer_mode(WoDev* dev) { return dev ? dev->peer_mode : -1; }
@@ -3629,8 +3750,11 @@ static int ranks_render_assemble(WoDev* const* devs, uint32_t n, WoFrame fr, int
 // The draw_frame pipeline over n ranks: the frame is assembled into the slot's
 // device frame on the root's stream and then presented as for one device.
 extern "C" int wo_dev_frame_submit_ranks(WoDev* const* devs, uint32_t n, WoFrame const* frame, int slot,
-                                         long long* const* d_accum, uint32_t accum_spp, char* err, size_t errlen) {
-    if (n <= 1u) return wo_dev_frame_submit(devs[0], frame, slot, d_accum ? d_accum[0] : nullptr, accum_spp, err, errlen);
+                                         long long* const* d_accum, uint32_t accum_spp, int map_float, char* err,
+                                         size_t errlen) {
+    if (n <= 1u)
+        return wo_dev_frame_submit(devs[0], frame, slot, d_accum ? d_accum[0] : nullptr, accum_spp, map_float, err,
+                                   errlen);
     if (!present_slot_ok(slot)) {
         snprintf(err, errlen, "bad frame slot %d", slot);
         return -1;
@@ -3642,10 +3766,11 @@ extern "C" int wo_dev_frame_submit_ranks(WoDev* const* devs, uint32_t n, WoFrame
         return -1;
     }
     if (prep_slot(root, slot, frame->width, frame->height, frame->height, err, errlen)) return -1;
+    if (open_slot(root, slot, err, errlen)) return -1;
     if (ranks_render_assemble(devs, n, *frame, slot, d_accum, accum_spp, root->stream, root->d_slot[slot], false, err,
                               errlen))
         return -1;
-    return present_slot(root, slot, (size_t)frame->width * frame->height, err, errlen);
+    return present_slot(root, slot, (size_t)frame->width * frame->height, map_float != 0, err, errlen);
 }
 
 extern "C" int wo_dev_frame_ranks_device(WoDev* const* devs, uint32_t n, WoFrame const* frame, int slot, void* d_frame,
@@ -3708,7 +3833,7 @@ extern "C" int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, uint3
         set_err(err, errlen, "frame wait", e);
         return -1;
     }
-    *host = dev->h_slot[slot];
+    *host = dev->slot_float[slot] ? dev->h_slot[slot] : nullptr;  // NULL: wo_dev_frame_map_float on demand
     if (host_bgra8) *host_bgra8 = dev->h_bgra[slot];
     return 0;
 }

@@ -79,18 +79,21 @@ int wo_dev_launch_ex(WoDev* dev, WoFrame const* frame, void* d_out, void* stream
 int wo_dev_accum_prepare(WoDev* dev, uint32_t width, uint32_t height, uint32_t tile_rows, uint32_t nranks, int reset,
                          long long** d_accum, char* err, size_t errlen);
 /* The draw_frame pipeline: render a whole frame into frame slot 0 or 1 (with
- * accumulation when d_accum), encode it for present (sRGB, B8G8R8A8), copy both
- * to the slot's pinned host buffers and record the slot's event -- all
- * asynchronous on the device stream. */
+ * accumulation when d_accum) on the device stream; then, on the device's copy
+ * stream once the render is done, encode it for present (sRGB, B8G8R8A8), copy
+ * the encode (and the float frame when `map_float`) to the slot's pinned host
+ * buffers and record the slot's event.  Asynchronous; the next frame's render
+ * does not wait for the map-back. */
 int wo_dev_frame_submit(WoDev* dev, WoFrame const* frame, int slot, long long* d_accum, uint32_t accum_spp,
-                        char* err, size_t errlen);
+                        int map_float, char* err, size_t errlen);
 /* wo_dev_frame_submit over n ranks, devs[0] presenting: rank i renders its
  * row-cyclic 4-row tiles on devs[i] (d_accum[i]: its accumulation, or d_accum
  * NULL), ranks 1..n-1 copy their shares to devs[0] (peer DMA when the devices
  * differ), devs[0] assembles the frame into the slot.  Asynchronous; wait with
  * wo_dev_frame_wait(devs[0], slot, ...). */
 int wo_dev_frame_submit_ranks(WoDev* const* devs, uint32_t n, WoFrame const* frame, int slot,
-                              long long* const* d_accum, uint32_t accum_spp, char* err, size_t errlen);
+                              long long* const* d_accum, uint32_t accum_spp, int map_float, char* err,
+                              size_t errlen);
 /* A frame over n ranks rendered and assembled into the caller's device frame
  * d_frame (width x height float4, on devs[0]'s device), ordered on `stream`
  * (a stream of devs[0]'s device): the ranks render on their own streams once
@@ -133,10 +136,21 @@ int wo_jit_disk_store(const char* key_hex, const void* code, size_t size);
  * device's specialised kernel was loaded from. */
 int wo_dev_jit_origin(WoDev* dev, double* seconds);
 int wo_dev_lanes_info(WoDev* dev, uint32_t* out);
-/* Wait for the slot's frame; *host = its pixels (RGBA float), *host_bgra8 (if
- * non-NULL) = its present encode; both valid until the slot is submitted again. */
+/* Wait for the slot's frame; *host = its pixels (RGBA float; NULL when the
+ * submit did not map them back), *host_bgra8 (if non-NULL) = its present
+ * encode; both valid until the slot is submitted again. */
 int wo_dev_frame_wait(WoDev* dev, int slot, float const** host, uint32_t const** host_bgra8, char* err,
                       size_t errlen);
+/* The float pixels of a waited-for slot, copied from the device now if the
+ * submit left them there (synchronous). */
+int wo_dev_frame_map_float(WoDev* dev, int slot, float const** host, char* err, size_t errlen);
+/* Pipeline timestamps of present-slot frames (on: from now; see
+ * wo_renderer_frame_stamps).  slot_stamps: the slot's last frame, ms after the
+ * stamps were turned on: render begin, render end, map-back end; -1 if none. */
+int wo_dev_set_stamps(WoDev* dev, int on, char* err, size_t errlen);
+int wo_dev_slot_stamps(WoDev* dev, int slot, double out[3]);
+/* Drain every stream of the device. */
+int wo_dev_sync(WoDev* dev);
 /* Present encode of `pixels` float4 pixels into B8G8R8A8 sRGB (present.c) on
  * the current device, async on `stream`. */
 int wo_dev_srgb8(void const* d_rgba, void* d_bgra8, size_t pixels, void* stream, char* err, size_t errlen);

@@ -97,9 +97,16 @@ struct Wo_Renderer {
     int pending[2];
     uint32_t pend_w[2], pend_h[2];
     uint64_t frame_seq;
-    float const* last_frame;
+    float const* last_frame;     /* NULL until mapped back (lazily, wo_renderer_last_frame) */
     uint32_t const* last_bgra8;  /* its present encode (B8G8R8A8 sRGB) */
     uint32_t last_w, last_h;
+    int last_slot;               /* the presented frame's slot (-1: none) */
+    int map_float;               /* copy every presented float frame to the host (else on demand) */
+    /* pipeline timestamps (wo_renderer_set_frame_stamps): per presented frame,
+     * render begin / render end / map-back end in ms */
+    int stamps;
+    uint32_t n_stamps;
+    double stamp_log[256][3];
 };
 
 /* scene_compile.c */

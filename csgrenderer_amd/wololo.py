@@ -122,6 +122,9 @@ SIGNATURES = {
     "wo_renderer_finish": (c_int, [c_void_p]),
     "wo_renderer_last_frame": (POINTER(c_float), [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
     "wo_renderer_last_frame_bgra8": (POINTER(c_uint32), [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
+    "wo_renderer_set_map_float": (None, [c_void_p, c_int]),
+    "wo_renderer_set_frame_stamps": (c_int, [c_void_p, c_int]),
+    "wo_renderer_frame_stamps": (c_int, [c_void_p, POINTER(c_double), c_int]),
     "wo_srgb8_thresholds": (None, [POINTER(c_float)]),
     "wo_srgb8_encode_device": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "wo_srgb8_encode_host": (None, [c_void_p, c_void_p, c_size_t]),
@@ -415,6 +418,22 @@ class Renderer:
         if not p:
             return None
         return np.ctypeslib.as_array(p, shape=(h.value * w.value,)).reshape(h.value, w.value).copy()
+
+    def set_map_float(self, every_frame: bool):
+        """Map every presented frame's float pixels back (True) or only when last_frame() asks (default)."""
+        self.lib.wo_renderer_set_map_float(self.ptr, 1 if every_frame else 0)
+
+    def set_frame_stamps(self, on: bool):
+        if self.lib.wo_renderer_set_frame_stamps(self.ptr, 1 if on else 0):
+            raise WololoError(last_error())
+
+    def frame_stamps(self):
+        """Logged pipeline stamps, a list of (render_begin, render_end, mapback_end) ms per presented frame."""
+        buf = (c_double * (3 * 256))()
+        n = self.lib.wo_renderer_frame_stamps(self.ptr, buf, 256)
+        if n < 0:
+            raise WololoError(last_error())
+        return [tuple(buf[3 * i:3 * i + 3]) for i in range(n)]
 
     def set_draw_params(self, params: RenderParams, pin_time: bool = True):
         self.lib.wo_renderer_set_draw_params(self.ptr, ctypes.byref(params), 1 if pin_time else 0)

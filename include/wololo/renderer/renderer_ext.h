@@ -135,15 +135,31 @@ int wo_renderer_take_segments(Wo_Renderer* r, unsigned long long* total);
 /* ---- frame pipeline and progressive rendering ----
  * The reference's draw_frame_with_renderer (renderer.c:2085-2219) ends every
  * frame with vkQueueWaitIdle (2212).  wo_renderer_draw_frame instead submits
- * frame k (render + copy to pinned host memory, asynchronous) and then waits
- * for and presents frame k-1: the GPU renders while the host presents, one
- * frame of latency.  Presenting = the last frame below, plus a PPM dump when
- * WOLOLO_OUTPUT names a file. */
+ * frame k (asynchronous: the render on the device's render stream; the map-back
+ * -- present encode and its copy to pinned host memory -- on a copy stream once
+ * the render is done, so frame k+1's render never waits for frame k's copies)
+ * and then waits for and presents frame k-1: the GPU renders while the host
+ * presents, one frame of latency.  Presenting = the last frame below, plus a PPM
+ * dump when WOLOLO_OUTPUT names a file. */
 /* Wait for and present every submitted frame.  0, or -1 (last_error). */
 int wo_renderer_finish(Wo_Renderer* r);
 /* Host pixels of the last presented frame (RGBA float, row 0 = top; NULL
- * before the first), valid until the next draw_frame / finish. */
+ * before the first), valid until the next draw_frame / finish.  The float frame
+ * is copied from the device on the first call after a present (unless
+ * wo_renderer_set_map_float asks for every frame), so a caller that only
+ * presents never pays for its 16 bytes per pixel of map-back. */
 float const* wo_renderer_last_frame(Wo_Renderer* r, uint32_t* width, uint32_t* height);
+/* every_frame != 0: map each presented frame's float pixels back with its
+ * present encode (asynchronously, on the copy stream); 0 (default): on demand. */
+void wo_renderer_set_map_float(Wo_Renderer* r, int every_frame);
+/* Pipeline timestamps (diagnostics): while on, each frame draw_frame presents
+ * logs three times in ms after the call that turned them on -- render begin,
+ * render end (both on the render stream) and map-back end (copy stream).
+ * set: 0 or -1 (drains the pipeline first); frame_stamps copies up to
+ * max_frames logged frames (oldest first, 3 doubles each) into out, empties the
+ * log and returns how many, or -1.  The log holds 256 frames. */
+int wo_renderer_set_frame_stamps(Wo_Renderer* r, int on);
+int wo_renderer_frame_stamps(Wo_Renderer* r, double* out, int max_frames);
 /* Present encode of the last presented frame: B8G8R8A8 sRGB, one uint32 per
  * pixel (B in the low byte) -- the reference's preferred swapchain format
  * (renderer.c:813-832) -- made on the GPU by wo_srgb8_encode_device.  Same

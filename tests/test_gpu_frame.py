@@ -422,3 +422,40 @@ def test_scene_edit_does_not_stall_draw_frame():
     _cmp(r.last_frame(), r.render(p), "two quick edits")
     assert wl.last_error() == ""
     r.close()
+
+
+@pytest.mark.parametrize("map_float", [False, True])
+def test_draw_frame_map_back_overlaps_the_next_render(map_float):
+    """frame k's map-back (present encode + D2H, on the copy
+    stream) must not hold back frame k+1's render.  The pipeline's own timing events
+    (wo_renderer_set_frame_stamps) show frame k+1's render beginning before frame k's
+    map-back has ended -- impossible when both sit on one stream, as they did through
+    round 3 -- and the presented frames stay bit-exact, with the float frame mapped
+    back lazily (default) or with every present (set_map_float)."""
+    r = wl.Renderer("mapback", max_nodes=4096)
+    info = scenes.build("csg32", r)
+    p = info.params(width=1920, height=1080, spp=16, seed=5)
+    r.set_draw_params(p)
+    r.set_map_float(map_float)
+    r.draw_frame()
+    r.finish()  # scene upload and kernel load out of the way
+    r.set_frame_stamps(True)
+    frames = 12
+    for _ in range(frames):
+        r.draw_frame()
+    r.finish()
+    st = r.frame_stamps()
+    assert len(st) == frames
+    for b, e, m in st:
+        assert b <= e <= m, st
+    overlapped = sum(1 for k in range(1, frames - 1) if st[k + 1][0] < st[k][2])
+    gaps = [st[k + 1][0] - st[k][1] for k in range(1, frames - 1)]
+    print(f"map_float={map_float}: render {np.mean([e - b for b, e, _ in st]):.3f} ms, map-back "
+          f"{np.mean([m - e for _, e, m in st]):.3f} ms, render gap {np.median(gaps):.4f} ms, "
+          f"{overlapped}/{frames - 2} next renders began inside the map-back")
+    assert overlapped >= (frames - 2) // 2, st
+    r.set_frame_stamps(False)
+    _cmp(r.last_frame(), r.render(p), f"presented frame (map_float={map_float})")
+    b8 = r.last_frame_bgra8()
+    assert np.array_equal(b8, wl.srgb8_encode_host(r.render(p)))
+    r.close()
