@@ -17,7 +17,7 @@ run() {
     local name="$1"
     shift
     timeout -k 10 300 rocprofv3 "$@" -d "$out/$name" -o "$name" --output-format csv -- \
-        python3 bench.py --no-cpu-baseline --no-count-work "${BENCH_ARGS[@]}" > "$out/$name.log" 2>&1
+        python3 bench.py --no-cpu-baseline --no-count-work --no-draw-frame --side-scenes "" "${BENCH_ARGS[@]}" > "$out/$name.log" 2>&1
     local rc=$?
     echo "[$tag/$name] rc=$rc"
     return $rc
