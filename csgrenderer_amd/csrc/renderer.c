@@ -107,10 +107,8 @@ Wo_Renderer* wo_renderer_new(Wo_App* app, char const* name, size_t max_node_coun
     r->dirty = 1;
     r->view_version++;
     {
-        const char* j = getenv("WOLOLO_JIT");
         const char* t = getenv("WOLOLO_TRACER");
         r->tracer = WO_TRACER_AUTO;
-        if (j && strcmp(j, "0") == 0) r->tracer = WO_TRACER_INTERPRETER;
         if (t && strcmp(t, "interpreter") == 0) r->tracer = WO_TRACER_INTERPRETER;
         if (t && strcmp(t, "jit") == 0) r->tracer = WO_TRACER_JIT;
         if (t && strcmp(t, "lanes") == 0) r->tracer = WO_TRACER_LANES;

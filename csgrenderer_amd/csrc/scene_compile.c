@@ -19,7 +19,7 @@
  *      when the subtrahend is emitted first;
  *   4. every maximal union cluster is re-bracketed as a bounding-volume hierarchy
  *      over its operands (regroup; union is associative and commutative);
- *   5. subtrees with >= 2 leaves (WOLOLO_BOUND_MIN_LEAVES) and a finite extent get a conservative
+ *   5. subtrees with >= 2 leaves and a finite extent get a conservative
  *      WO_OP_BOUND sphere so a wave whose rays all miss can skip them.
  */
 #include <math.h>
@@ -61,9 +61,6 @@ typedef struct Ctx {
     size_t errlen;
     int failed;
     int bound_min_leaves; /* smallest subtree (in leaves) that gets a BOUND record */
-    int regroup_unions;   /* rebuild union clusters as a BVH (WOLOLO_REGROUP_UNIONS=0: keep the scene's) */
-    int bvh_sah;          /* split by surface-area cost (WOLOLO_BVH_SAH=0: at the median) */
-    int small_spheres_first; /* convex members: spheres by ascending radius (WOLOLO_MEMBER_ORDER=0: scene order) */
 } Ctx;
 
 #define MAX_EXPANDED_NODES (1u << 21)
@@ -639,7 +636,7 @@ static int regroup(Ctx* c, int id) {
         for (int i = 0; i < nb; ++i) ops[i] = tmp[i].id;
         nb = kept;
     }
-    int root = nb ? bvh_build(c, ops, nb, tmp, c->bvh_sah && nb >= 16) : -1;
+    int root = nb ? bvh_build(c, ops, nb, tmp, nb >= 16) : -1;
     /* giant and unbounded operands go first in the program (postfix order), so a
      * traversal meets a ground plane or sphere -- the likely nearest hit of a
      * downward ray -- before the hierarchy it may then prune */
@@ -739,7 +736,7 @@ static void emit(Ctx* c, int id, double outer_r) {
             free(mem);
             return;
         }
-        if (c->small_spheres_first) {
+        {
             /* the sphere members in ascending radius (stable; half-spaces keep their
              * slots, so slab face pairs stay adjacent): the kernels skip a primitive's
              * later members once its interval is empty on a whole wave, and the
@@ -788,25 +785,6 @@ int wo_compile_scene(Wo_Renderer* r, char* err, size_t errlen) {
     c.err = err;
     c.errlen = errlen;
     c.bound_min_leaves = 2;
-    c.regroup_unions = 1;
-    c.bvh_sah = 1;
-    c.small_spheres_first = 1;
-    {
-        const char* v = getenv("WOLOLO_MEMBER_ORDER");
-        if (v && *v) c.small_spheres_first = v[0] != '0';
-    }
-    {
-        const char* v = getenv("WOLOLO_BVH_SAH");
-        if (v && strcmp(v, "0") == 0) c.bvh_sah = 0;
-    }
-    {
-        const char* v = getenv("WOLOLO_REGROUP_UNIONS");
-        if (v && strcmp(v, "0") == 0) c.regroup_unions = 0;
-    }
-    {
-        const char* v = getenv("WOLOLO_BOUND_MIN_LEAVES");
-        if (v && *v) c.bound_min_leaves = atoi(v) > 1 ? atoi(v) : 2;
-    }
 
     int* roots = (int*)malloc(sizeof(int) * (r->node_count ? r->node_count : 1));
     if (!roots) {
@@ -825,7 +803,7 @@ int wo_compile_scene(Wo_Renderer* r, char* err, size_t errlen) {
     }
     if (!c.failed && nroots > 0) {
         int root = make_union(&c, roots, nroots);
-        if (root >= 0 && !c.failed && c.regroup_unions) root = regroup(&c, root);
+        if (root >= 0 && !c.failed) root = regroup(&c, root);
         if (root >= 0 && !c.failed) {
             analyse(&c, root);
             if (c.e[root].need > 31) fail(&c, "CSG tree needs an evaluation stack deeper than 31");

@@ -78,19 +78,6 @@ static void emit_consts(Buf* b, int indent, const char* type, const char* names[
     bput(b, ");\n");
 }
 
-/* The same as VGPR moves (term mode's event-key constants: they end up in the
- * low half of a VGPR key pair anyway, and as SGPRs they pushed other scalars into
- * lane spills read back on every trace) */
-static void emit_vconsts(Buf* b, int indent, const char* type, const char* names[], const uint32_t* vals, int n) {
-    bput(b, "%*s%s %s", indent, "", type, names[0]);
-    for (int i = 1; i < n; ++i) bput(b, ", %s", names[i]);
-    bput(b, ";\n%*sasm volatile(\"", indent, "");
-    for (int i = 0; i < n; ++i) bput(b, "%sv_mov_b32 %%%d, 0x%08x", i ? "\\n\\t" : "", i, vals[i]);
-    bput(b, "\" : ");
-    for (int i = 0; i < n; ++i) bput(b, "%s\"=v\"(%s)", i ? ", " : "", names[i]);
-    bput(b, ");\n");
-}
-
 typedef struct Gen {
     const WoRec* prog;
     uint32_t n;
@@ -100,25 +87,11 @@ typedef struct Gen {
     uint32_t nbound;  /* BOUND counter (cull flag names) */
     int first_pass;   /* gen_collect: the first pass (cull tests, bits at t_min) or a re-collect */
     uint32_t nval;    /* value counter (eval temporaries) */
-    int flat_eval;    /* gen_eval_flat: literal sets tested with one mask compare */
-    int axis_pairs;   /* consecutive opposite faces on one axis fused (axis_pair_meet) */
-    int bound_single; /* BOUND records around a single primitive tested too */
-    int member_skip;  /* members after the first skipped when the interval is empty on every lane */
-    int pair_window;  /* LDS event list behind two register slots (PairLdsWindow) */
-    int lit_consts;   /* sphere / BOUND / axis-face constants as VALU literal operands instead of scalar moves */
     int first_event;  /* the first event of waves that start outside every primitive from a constant table */
-    int fused_sphere; /* a lone sphere's membership and events inside its sqrt branch (no empty interval) */
-    int dl_eval;      /* chains of literal sets evaluated as decision lists (gen_eval_flat) */
     int term_mode;    /* root a union of <= 2-literal conjunctions: term transitions, no event window (gen_term) */
-    int union_count;  /* root a union of literal sets: a count of true terms kept per event */
     int spatial;      /* collect grouped by a spatial hierarchy over the primitives (gen_spatial) */
-    int spatial_sah;  /* its splits by least surface area instead of at the median */
     uint32_t spatial_leaf; /* most primitives in a leaf group of that hierarchy */
-    double spatial_ct;     /* group-test cost for SAH leaf decisions (0: split down to spatial_leaf) */
-    int dist_cull;         /* term mode, first pass: skip a group whose sphere begins beyond every lane's best transition */
-    int key_vmov;          /* term mode: event-key constants by v_mov (VGPRs) instead of s_mov */
-    int term_dist;         /* term mode: a lone sphere / a pair's second literal skipped by lanes whose best precedes it */
-    int cull_barrier;      /* cull[] through an opaque move: 1 in re-collects and sweep steps, 2 re-collects only (WOLOLO_JIT_CULL_BARRIER) */
+    int cull_barrier;      /* cull[] through an opaque move in re-collects */
     uint32_t ncw;          /* words of cull[] */
     struct SPrim* sprims;  /* the bounded primitives it groups */
     uint32_t nsprims;
@@ -129,14 +102,14 @@ typedef struct Gen {
     int err;
 } Gen;
 
-/* A BOUND record gets a wave-level test when its subtree has enough leaves, and
- * (bound_single off) when it holds more than one primitive: a lone convex
- * primitive's own first member, with the member skip, is the cheaper test. */
+/* A BOUND record gets a wave-level test when its subtree has enough leaves and
+ * holds more than one primitive: a lone convex primitive's own first member,
+ * with the member skip, is the cheaper test (csg32 4.87 -> 4.82 ms). */
 static int bound_tested(const Gen* g, uint32_t pc) {
     const WoRec* r = &g->prog[pc];
     if (g->spatial) return 0; /* the spatial hierarchy culls instead (gen_spatial) */
     if (r->u1 < g->bound_min_leaves) return 0;
-    if (!g->bound_single && pc + 1u < g->n && g->prog[pc + 1u].op == WO_OP_PRIM &&
+    if (pc + 1u < g->n && g->prog[pc + 1u].op == WO_OP_PRIM &&
         pc + 2u + g->prog[pc + 1u].u0 == r->u0)
         return 0;
     return 1;
@@ -155,61 +128,45 @@ static void gen_members(Gen* g, uint32_t pc, uint32_t cnt, int indent) {
         const WoRec* L = &g->prog[pc + 1 + m];
         uint32_t vl[4];
         for (int i = 0; i < 4; ++i) vl[i] = fbits(L->f[i]);
-        if (m > 0 && g->member_skip) /* empty on every lane: the other members cannot widen it */
+        if (m > 0) /* empty on every lane: the other members cannot widen it */
             bput(g->b, "%*s  if (__ballot(!(iv.a > iv.b)) != 0ull) {\n", indent, ""), ++open_skips;
         bput(g->b, "%*s  {\n", indent, "");
         const WoRec* L2 = m + 1u < cnt ? &g->prog[pc + 2 + m] : NULL;
-        if (g->axis_pairs && L->op == WO_LEAF_HALFSPACE && L->u1 != 0u && L2 && L2->op == WO_LEAF_HALFSPACE &&
+        if (L->op == WO_LEAF_HALFSPACE && L->u1 != 0u && L2 && L2->op == WO_LEAF_HALFSPACE &&
             L2->u1 == L->u1 && (L->f[L->u1 - 1u] > 0.0f) != (L2->f[L2->u1 - 1u] > 0.0f)) {
             /* two faces of a slab: one entry, one exit (axis_pair_meet) */
-            static const char* nh[2] = {"c3", "c3b"};
             static const char axis[3] = {'x', 'y', 'z'};
             const char ax = axis[L->u1 - 1u];
             const int pos = L->f[L->u1 - 1u] > 0.0f; /* s1 = +1 */
             uint32_t vh[2] = {vl[3], fbits(L2->f[3])};
             bput(g->b, "%*s    WO_WK_N(WO_WORK_HALFSPACE_TESTS, 2u);\n", indent, "");
             if (m == 0) bput(g->b, "%*s    wodev::ivl_open(iv);\n", indent, "");
-            if (g->lit_consts) {
-                /* dist1 = h1 - s1*oa, dist2 = h2 + s1*oa with h as a literal operand */
-                bput(g->b,
-                     "%*s    float dist1, dist2;\n"
-                     "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist1) : \"v\"(o.%c));\n"
-                     "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist2) : \"v\"(o.%c));\n"
-                     "%*s    wodev::axis_pair_meet_d(iv, %s, dist1, dist2, d.%c, iv%c, %uu, %uu);\n%*s  }\n",
-                     indent, "", indent, "", pos ? "v_sub_f32_e32" : "v_add_f32_e32", vh[0], ax, indent, "",
-                     pos ? "v_add_f32_e32" : "v_sub_f32_e32", vh[1], ax, indent, "", pos ? "1.0f" : "-1.0f", ax,
-                     ax, m, m + 1u, indent, "");
-            } else {
-                emit_consts(g->b, indent + 4, "float", nh, vh, 2);
-                bput(g->b,
-                     "%*s    wodev::axis_pair_meet(iv, %s, c3, c3b, o.%c, d.%c, iv%c, %uu, %uu);\n%*s  }\n",
-                     indent, "", pos ? "1.0f" : "-1.0f", ax, ax, ax, m, m + 1u, indent, "");
-            }
+            /* dist1 = h1 - s1*oa, dist2 = h2 + s1*oa with h as a literal operand */
+            bput(g->b,
+                 "%*s    float dist1, dist2;\n"
+                 "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist1) : \"v\"(o.%c));\n"
+                 "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist2) : \"v\"(o.%c));\n"
+                 "%*s    wodev::axis_pair_meet_d(iv, %s, dist1, dist2, d.%c, iv%c, %uu, %uu);\n%*s  }\n",
+                 indent, "", indent, "", pos ? "v_sub_f32_e32" : "v_add_f32_e32", vh[0], ax, indent, "",
+                 pos ? "v_add_f32_e32" : "v_sub_f32_e32", vh[1], ax, indent, "", pos ? "1.0f" : "-1.0f", ax,
+                 ax, m, m + 1u, indent, "");
             ++m;
             continue;
         }
         bput(g->b, "%*s    WO_WK(%s);\n", indent, "",
              L->op == WO_LEAF_SPHERE ? "WO_WORK_SPHERE_TESTS" : "WO_WORK_HALFSPACE_TESTS");
         if (L->op == WO_LEAF_HALFSPACE && L->u1 != 0u) {
-            /* axis-aligned: s = +-1 stays a literal (inline constant), h in an SGPR */
-            static const char* nh[1] = {"c3"};
+            /* axis-aligned: s = +-1 stays a literal (inline constant), h a literal operand */
             static const char axis[3] = {'x', 'y', 'z'};
             char ax = axis[L->u1 - 1u];
             const int pos = L->f[L->u1 - 1u] > 0.0f;
-            if (g->lit_consts) {
-                bput(g->b,
-                     "%*s    float dist;\n"
-                     "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist) : \"v\"(o.%c));\n"
-                     "%*s    wodev::halfspace_axis_dist(%s, dist, d.%c, iv%c, la, lb);\n",
-                     indent, "", indent, "", pos ? "v_sub_f32_e32" : "v_add_f32_e32", vl[3], ax, indent, "",
-                     pos ? "1.0f" : "-1.0f", ax, ax);
-            } else {
-                emit_consts(g->b, indent + 4, "float", nh, &vl[3], 1);
-                bput(g->b,
-                     "%*s    wodev::halfspace_axis_interval(%s, c3, o.%c, d.%c, iv%c, la, lb);\n",
-                     indent, "", pos ? "1.0f" : "-1.0f", ax, ax, ax);
-            }
-        } else if (L->op == WO_LEAF_SPHERE && g->lit_consts) {
+            bput(g->b,
+                 "%*s    float dist;\n"
+                 "%*s    asm(\"%s %%0, 0x%08x, %%1\" : \"=v\"(dist) : \"v\"(o.%c));\n"
+                 "%*s    wodev::halfspace_axis_dist(%s, dist, d.%c, iv%c, la, lb);\n",
+                 indent, "", indent, "", pos ? "v_sub_f32_e32" : "v_add_f32_e32", vl[3], ax, indent, "",
+                 pos ? "1.0f" : "-1.0f", ax, ax);
+        } else if (L->op == WO_LEAF_SPHERE) {
             /* the centre and r^2 as VALU literal operands: o - c and r^2 - ll
              * are single VOP2 operations (the constant needs no scalar move) */
             bput(g->b,
@@ -222,11 +179,9 @@ static void gen_members(Gen* g, uint32_t pc, uint32_t cnt, int indent) {
                  "%*s    wodev::sphere_interval_bd(b, disc, la, lb);\n",
                  indent, "", indent, "", vl[0], indent, "", vl[1], indent, "", vl[2], indent, "", indent, "",
                  vl[3], indent, "");
-        } else {
+        } else { /* a general half-space: its constants by scalar moves */
             emit_consts(g->b, indent + 4, "float", nl, vl, 4);
-            bput(g->b,
-                 "%*s    wodev::%s_interval(c0, c1, c2, c3, o, d, la, lb);\n",
-                 indent, "", L->op == WO_LEAF_SPHERE ? "sphere" : "halfspace");
+            bput(g->b, "%*s    wodev::halfspace_interval(c0, c1, c2, c3, o, d, la, lb);\n", indent, "");
         }
         if (m == 0)
             bput(g->b, "%*s    wodev::ivl_first(iv, la, lb);\n", indent, "");
@@ -244,36 +199,27 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
         if (r->op == WO_OP_BOUND && !bound_tested(g, pc)) {
             ++pc; /* too small to pay for a wave-level test: the subtree is emitted inline */
         } else if (r->op == WO_OP_BOUND) {
-            static const char* nb[5] = {"bc0", "bc1", "bc2", "bc3", "bc4"};
             uint32_t vb[5];
             for (int i = 0; i < 5; ++i) vb[i] = fbits(r->f[i]);
             uint32_t k = g->nbound++;
             if (g->first_pass) { /* the wave's cull decision; re-collects reuse it */
                 bput(g->b, "%*s{  // BOUND %u\n%*s  WO_WK(WO_WORK_BOUND_TESTS);\n", indent, "", k, indent, "");
-                if (g->lit_consts) {
-                    /* c - o and tca + R with the constants as VALU literal operands; R^2
-                     * (an FMA addend) in an SGPR */
-                    static const char* nr[1] = {"bc3"};
-                    emit_consts(g->b, indent + 2, "float", nr, &vb[3], 1);
-                    bput(g->b,
-                         "%*s  float ox, oy, oz, tca, d2, tr;\n"
-                         "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(ox) : \"v\"(o.x));\n"
-                         "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oy) : \"v\"(o.y));\n"
-                         "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oz) : \"v\"(o.z));\n"
-                         "%*s  wodev::bound_tca_d2(ox, oy, oz, d, tca, d2);\n"
-                         "%*s  asm(\"v_add_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(tr) : \"v\"(tca));\n"
-                         "%*s  const bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, bc3)) | (tr < 0.0f);\n"
-                         "%*s  if (__ballot(!miss) == 0ull) cull[%u] |= %uu;\n"
-                         "%*s}\n",
-                         indent, "", indent, "", vb[0], indent, "", vb[1], indent, "", vb[2], indent, "", indent, "",
-                         vb[4], indent, "", indent, "", k / 32, 1u << (k % 32), indent, "");
-                } else {
-                    emit_consts(g->b, indent + 2, "float", nb, vb, 5);
-                    bput(g->b,
-                         "%*s  if (__ballot(wodev::bound_may_hit(bc0, bc1, bc2, bc3, bc4, o, d)) == 0ull) cull[%u] |= %uu;\n"
-                         "%*s}\n",
-                         indent, "", k / 32, 1u << (k % 32), indent, "");
-                }
+                /* c - o and tca + R with the constants as VALU literal operands; R^2
+                 * (an FMA addend) in an SGPR */
+                static const char* nr[1] = {"bc3"};
+                emit_consts(g->b, indent + 2, "float", nr, &vb[3], 1);
+                bput(g->b,
+                     "%*s  float ox, oy, oz, tca, d2, tr;\n"
+                     "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(ox) : \"v\"(o.x));\n"
+                     "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oy) : \"v\"(o.y));\n"
+                     "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oz) : \"v\"(o.z));\n"
+                     "%*s  wodev::bound_tca_d2(ox, oy, oz, d, tca, d2);\n"
+                     "%*s  asm(\"v_add_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(tr) : \"v\"(tca));\n"
+                     "%*s  const bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, bc3)) | (tr < 0.0f);\n"
+                     "%*s  if (__ballot(!miss) == 0ull) cull[%u] |= %uu;\n"
+                     "%*s}\n",
+                     indent, "", indent, "", vb[0], indent, "", vb[1], indent, "", vb[2], indent, "", indent, "",
+                     vb[4], indent, "", indent, "", k / 32, 1u << (k % 32), indent, "");
             }
             bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
             gen_collect(g, pc + 1, r->u0, indent + 2);
@@ -283,7 +229,7 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
             uint32_t ord = r->u1, cnt = r->u0;
             static const char* nk[2] = {"ka", "kb"};
             bput(g->b, "%*s{  // primitive %u (%u leaves)\n", indent, "", ord, cnt);
-            if (cnt == 1u && g->fused_sphere && g->lit_consts && g->prog[pc + 1].op == WO_LEAF_SPHERE) {
+            if (cnt == 1u && g->prog[pc + 1].op == WO_LEAF_SPHERE) {
                 gen_lone_sphere(g, &g->prog[pc + 1], ord, indent);
                 pc += 2;
                 continue;
@@ -459,14 +405,6 @@ static void gen_spatial(Gen* g, SPrim* p, uint32_t n, int indent, int root) {
             static const char* nr[1] = {"bc3"};
             uint32_t nprim = 0;
             for (uint32_t i = 0; i < n; ++i) nprim += p[i].npc ? p[i].npc : 1u;
-            /* term mode: in the first pass a group none of whose lanes can find a transition
-             * before its best so far is skipped as well (not marked culled: the re-collect
-             * pass looks after that best).  Every transition of a term lies inside its
-             * positive literal, inside the group's sphere, so at or after tca - R (less a
-             * slack above tca's rounding: |o - c| <= |tca| + R for a ray that meets the
-             * sphere); a group that begins beyond t_min holds no term at t_min either. */
-            const int dc = g->term_mode && g->dist_cull;
-            if (dc) bput(g->b, "%*sbool gskip%u;\n", indent, "", k);
             bput(g->b, "%*s{  // group %u (%u primitives)\n%*s  WO_WK(WO_WORK_BOUND_TESTS);\n", indent, "", k, nprim,
                  indent, "");
             emit_consts(g->b, indent + 2, "float", nr, &vr2, 1);
@@ -481,31 +419,20 @@ static void gen_spatial(Gen* g, SPrim* p, uint32_t n, int indent, int root) {
                  "%*s  if (__ballot(!miss) == 0ull) cull[%u] |= %uu;\n",
                  indent, "", indent, "", fbits(fc[0]), indent, "", fbits(fc[1]), indent, "", fbits(fc[2]), indent, "",
                  indent, "", fbits(fR), indent, "", indent, "", k / 32, 1u << (k % 32));
-            if (!dc) bput(g->b, "%*s}\n", indent, "");
-            if (dc) {
-                bput(g->b,
-                     "%*s  float lo0;\n"
-                     "%*s  asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(lo0) : \"v\"(tca));\n"
-                     "%*s  const bool far = __builtin_fmaf(-1e-5f, tr, lo0) > __uint_as_float((uint32_t)(best >> 32));\n"
-                     "%*s  gskip%u = __ballot(!miss & !far) == 0ull;\n"
-                     "%*s}\n",
-                     indent, "", indent, "", fbits(fR), indent, "", indent, "", k, indent, "");
-                bput(g->b, "%*sif (!gskip%u) {\n", indent, "", k);
-            } else {
-                bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
-            }
+            bput(g->b, "%*s}\n%*sif (!(cull[%u] & %uu)) {\n", indent, "", indent, "", k / 32, 1u << (k % 32));
         } else {
             bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
         }
         inner = indent + 2;
     }
-    /* with a group-test cost (WOLOLO_JIT_SPATIAL_CT = c > 0), a set of up to twice the
-     * leaf size stays one group unless the best split's expected cost, c + (R_l^2 n_l +
-     * R_r^2 n_r) / R^2 primitive tests, is below the n tests of a leaf */
-    int leaf = n <= g->spatial_leaf;
-    if (!leaf && g->spatial_ct > 0.0 && g->spatial_sah && n <= 2u * g->spatial_leaf) {
-        double c[3], R;
-        sprim_bound(p, n, c, &R);
+    if (n <= g->spatial_leaf) {
+        for (uint32_t i = 0; i < n; ++i) gen_sprim(g, &p[i], inner);
+    } else {
+        /* surface-area split (csg32 3.716 -> 3.586 ms against median splits): over
+         * the three axes (centres sorted) and every cut, the least R_left^2 * n_left
+         * + R_right^2 * n_right of the enclosing spheres */
+        uint32_t cut = n / 2u;
+        int ax = 0;
         double best = -1.0;
         for (int a = 0; a < 3; ++a) {
             qsort(p, n, sizeof(SPrim), a == 0 ? sprim_cmp0 : a == 1 ? sprim_cmp1 : sprim_cmp2);
@@ -514,38 +441,8 @@ static void gen_spatial(Gen* g, SPrim* p, uint32_t n, int indent, int root) {
                 sprim_bound(p, k, cl, &rl);
                 sprim_bound(p + k, n - k, cr, &rr);
                 const double cost = rl * rl * k + rr * rr * (n - k);
-                if (best < 0.0 || cost < best) best = cost;
+                if (best < 0.0 || cost < best) best = cost, ax = a, cut = k;
             }
-        }
-        leaf = g->spatial_ct + best / (R * R) >= (double)n;
-    }
-    if (leaf) {
-        for (uint32_t i = 0; i < n; ++i) gen_sprim(g, &p[i], inner);
-    } else {
-        uint32_t cut = n / 2u;
-        int ax = 0;
-        if (g->spatial_sah) {
-            /* surface-area split: over the three axes (centres sorted) and every cut,
-             * the least R_left^2 * n_left + R_right^2 * n_right of the enclosing spheres */
-            double best = -1.0;
-            for (int a = 0; a < 3; ++a) {
-                qsort(p, n, sizeof(SPrim), a == 0 ? sprim_cmp0 : a == 1 ? sprim_cmp1 : sprim_cmp2);
-                for (uint32_t k = 1; k < n; ++k) {
-                    double cl[3], cr[3], rl, rr;
-                    sprim_bound(p, k, cl, &rl);
-                    sprim_bound(p + k, n - k, cr, &rr);
-                    const double cost = rl * rl * k + rr * rr * (n - k);
-                    if (best < 0.0 || cost < best) best = cost, ax = a, cut = k;
-                }
-            }
-        } else {
-            /* median split along the longest axis of the centres */
-            double lo[3], hi[3];
-            for (int a = 0; a < 3; ++a) lo[a] = hi[a] = p[0].c[a];
-            for (uint32_t i = 0; i < n; ++i)
-                for (int a = 0; a < 3; ++a) lo[a] = fmin(lo[a], p[i].c[a]), hi[a] = fmax(hi[a], p[i].c[a]);
-            for (int a = 1; a < 3; ++a)
-                if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
         }
         qsort(p, n, sizeof(SPrim), ax == 0 ? sprim_cmp0 : ax == 1 ? sprim_cmp1 : sprim_cmp2);
         gen_spatial(g, p, cut, inner, 0);
@@ -767,26 +664,12 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
     if (q->npc > 1u) bput(g->b, " AND %sprimitive %u", pos[1] ? "" : "NOT ", g->prog[pcs[1]].u1);
     bput(g->b, "\n");
     const WoRec* P = &g->prog[pcs[0]];
-    if (q->npc == 1u && pos[0] && P->u0 == 1u && g->prog[pcs[0] + 1u].op == WO_LEAF_SPHERE && g->lit_consts) {
+    if (q->npc == 1u && pos[0] && P->u0 == 1u && g->prog[pcs[0] + 1u].op == WO_LEAF_SPHERE) {
         /* a lone sphere: its interval is [-b - s, -b + s] exactly when disc >= 0, so
          * its transitions are formed inside the branch that computes s */
         const WoRec* L = &g->prog[pcs[0] + 1u];
         uint32_t vl[4];
         for (int i = 0; i < 4; ++i) vl[i] = fbits(L->f[i]);
-        /* term_dist: a lane whose best transition so far precedes the sphere's entry
-         * cannot take one of its keys, and is not inside it at t_min.  s = sqrt(disc)
-         * <= R = fl(sqrt(r^2)) (disc <= r^2; the device's sqrt is correctly rounded,
-         * and so is a float's sqrt through double), so la = fl(-b - s) >= fl(-b - R)
-         * = -fl(b + R): the lane is skipped when fl(b + R) < -t_best (no best: NaN,
-         * never skipped).  Same keys, same image. */
-        char dist[256] = "";
-        if (g->term_dist) {
-            const float R = (float)sqrt((double)L->f[3]);
-            snprintf(dist, sizeof dist,
-                     "%*s  float bR;\n%*s  asm(\"v_add_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(bR) : \"v\"(b));\n"
-                     "%*s  const bool nearer = !(bR < -__uint_as_float((uint32_t)(best >> 32)));\n",
-                     indent, "", indent, "", fbits(R), indent, "");
-        }
         bput(g->b,
              "%*s  WO_WK(WO_WORK_SPHERE_TESTS);\n"
              "%*s  float fx, fy, fz, b, ll, disc;\n"
@@ -795,18 +678,16 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
              "%*s  asm(\"v_subrev_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(fz) : \"v\"(o.z));\n"
              "%*s  wodev::sphere_fbl(fx, fy, fz, d, b, ll);\n"
              "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(disc) : \"v\"(ll));\n"
-             "%s"
-             "%*s  if (__ballot(wodev::sphere_need(b, disc)%s) != 0ull) {\n"
+             "%*s  if (__ballot(wodev::sphere_need(b, disc)) != 0ull) {\n"
              "%*s    asm volatile(\"\");\n"
              "%*s    if (!(disc < 0.0f)) {\n"
              "%*s      const float s = wodev::sqrt_pt(disc), nb = -b, la = nb - s, lb = nb + s;\n"
              "%*s      uint32_t ka, kb;\n"
-             "%*s      asm volatile(\"%s %%0, 0x%08x\\n\\t%s %%1, 0x%08x\" : \"=%s\"(ka), \"=%s\"(kb));\n"
+             "%*s      asm volatile(\"s_mov_b32 %%0, 0x%08x\\n\\ts_mov_b32 %%1, 0x%08x\" : \"=s\"(ka), \"=s\"(kb));\n"
              "%*s      const uint64_t k0 = wodev::event_key_lo(la, ka), k1 = wodev::event_key_lo(lb, kb);\n",
              indent, "", indent, "", indent, "", vl[0], indent, "", vl[1], indent, "", vl[2], indent, "", indent, "",
-             vl[3], dist, indent, "", g->term_dist ? " & nearer" : "", indent, "", indent, "", indent, "", indent, "",
-             indent, "", g->key_vmov ? "v_mov_b32" : "s_mov_b32", o0 << 12, g->key_vmov ? "v_mov_b32" : "s_mov_b32",
-             (o0 << 12) | (1u << 11), g->key_vmov ? "v" : "s", g->key_vmov ? "v" : "s", indent, "");
+             vl[3], indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", o0 << 12,
+             (o0 << 12) | (1u << 11), indent, "");
         if (first) bput(g->b, "%*s      cnt += ((la <= tmin) & (lb > tmin)) ? 1u : 0u;\n", indent, "");
         bput(g->b,
              "%*s      WO_WK(WO_WORK_EVENTS);\n"
@@ -821,7 +702,7 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
     uint32_t vk[4] = {o0 << 12, (o0 << 12) | (1u << 11), 0u, 0u};
     static const char* nk[4] = {"ka0", "kb0", "ka1", "kb1"};
     if (q->npc == 1u) {
-        (g->key_vmov ? emit_vconsts : emit_consts)(g->b, indent + 2, "uint32_t", nk, vk, 2);
+        emit_consts(g->b, indent + 2, "uint32_t", nk, vk, 2);
         bput(g->b, "%*s  const wodev::TermLit x = wodev::term_lit(ia, ka0, kb0);\n", indent, "");
         if (first) bput(g->b, "%*s  cnt += %swodev::term_in0(x) ? 1u : 0u;\n", indent, "", pos[0] ? "" : "!");
         bput(g->b,
@@ -836,19 +717,13 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
     vk[2] = o1 << 12;
     vk[3] = (o1 << 12) | (1u << 11);
     /* a positive first literal empty along every lane's ray: the term is false throughout */
-    /* term_dist: every transition of the term lies inside its positive first literal,
-     * at or after ia.a, so a lane whose best precedes ia.a skips the second literal */
-    if (pos[0] && g->term_dist)
-        bput(g->b,
-             "%*s  if (__ballot(!(ia.a > ia.b) & (ia.b > tmin) & !(ia.a > __uint_as_float((uint32_t)(best >> 32)))) != 0ull) {\n",
-             indent, "");
-    else if (pos[0])
+    if (pos[0])
         bput(g->b, "%*s  if (__ballot(!(ia.a > ia.b) & (ia.b > tmin)) != 0ull) {\n", indent, "");
     else
         bput(g->b, "%*s  {\n", indent, "");
     bput(g->b, "%*s    wodev::Ivl ib;\n", indent, "");
     gen_term_ivl(g, pcs[1], "ib", indent + 4);
-    (g->key_vmov ? emit_vconsts : emit_consts)(g->b, indent + 4, "uint32_t", nk, vk, 4);
+    emit_consts(g->b, indent + 4, "uint32_t", nk, vk, 4);
     bput(g->b,
          "%*s    const wodev::TermLit x = wodev::term_lit(ia, ka0, kb0), y = wodev::term_lit(ib, ka1, kb1);\n",
          indent, "");
@@ -863,64 +738,6 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
          indent, "", indent, "", pos[0] ? "true" : "false", pos[1] ? "true" : "false", first ? "true" : "false",
          indent, "", pos[1] ? "true" : "false", pos[0] ? "true" : "false", first ? "true" : "false", indent, "",
          indent, "");
-}
-
-/* ---- eval: value of the subtree [start, end) as named 0/1 temporaries ---- */
-static uint32_t gen_eval(Gen* g, uint32_t start, uint32_t end, int indent) {
-    uint32_t stack[64];
-    int sp = 0;
-    uint32_t pc = start;
-    while (pc < end && !g->err) {
-        const WoRec* r = &g->prog[pc];
-        if (r->op == WO_OP_BOUND && !bound_tested(g, pc)) {
-            ++pc;
-        } else if (r->op == WO_OP_BOUND) {
-            uint32_t k = g->nbound++;
-            uint32_t v = g->nval++;
-            bput(g->b, "%*suint32_t v%u;\n%*sif (!(cull[%u] & %uu)) {\n", indent, "", v, indent, "", k / 32,
-                 1u << (k % 32));
-            uint32_t inner = gen_eval(g, pc + 1, r->u0, indent + 2);
-            bput(g->b, "%*s  v%u = v%u;\n%*s} else {\n%*s  v%u = 0u;\n%*s}\n", indent, "", v, inner, indent, "",
-                 indent, "", v, indent, "");
-            if (sp >= 64) {
-                g->err = 1;
-                return 0;
-            }
-            stack[sp++] = v;
-            pc = r->u0;
-        } else if (r->op == WO_OP_PRIM) {
-            uint32_t v = g->nval++;
-            bput(g->b, "%*suint32_t v%u = (bits[%u] >> %u) & 1u;\n", indent, "", v, r->u1 / 32, r->u1 % 32);
-            if (sp >= 64) {
-                g->err = 1;
-                return 0;
-            }
-            stack[sp++] = v;
-            pc += 1 + r->u0;
-        } else {
-            if (sp < 2) {
-                g->err = 1;
-                return 0;
-            }
-            uint32_t B = stack[--sp], A = stack[--sp];
-            uint32_t v = g->nval++;
-            const char* fmt = r->op == WO_OP_UNION   ? "%*suint32_t v%u = v%u | v%u;\n"
-                              : r->op == WO_OP_INTER ? "%*suint32_t v%u = v%u & v%u;\n"
-                              : r->op == WO_OP_DIFF  ? "%*suint32_t v%u = v%u & (v%u ^ 1u);\n"
-                                                     : NULL;
-            if (fmt)
-                bput(g->b, fmt, indent, "", v, A, B);
-            else /* RDIFF: B & ~A */
-                bput(g->b, "%*suint32_t v%u = v%u & (v%u ^ 1u);\n", indent, "", v, B, A);
-            stack[sp++] = v;
-            ++pc;
-        }
-    }
-    if (sp != 1) {
-        g->err = 1;
-        return 0;
-    }
-    return stack[0];
 }
 
 /* ---- eval, flattened: literal sets as one masked compare ----
@@ -987,7 +804,7 @@ static int term_is_literal(const Term* t) {
  * decides 0, else 1; a single literal takes the join's form) */
 static uint32_t dl_of(Gen* g, const Term* t, int kind) {
     if (t->dl) return t->dl;
-    if (!g->dl_eval || !t->kind || t->v != kNoName || !(t->P | t->N) || t->w >= DL_WORDS) return 0;
+    if (!t->kind || t->v != kNoName || !(t->P | t->N) || t->w >= DL_WORDS) return 0;
     const int k = term_is_literal(t) ? kind : t->kind;
     uint32_t id = dl_new(g);
     if (!id) return 0;
@@ -1503,129 +1320,34 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     g.n = n_recs;
     g.b = &b;
     uint32_t nw = n_prims ? (n_prims + 31u) / 32u : 1u;
-    /* Wave-level BOUND tests pay only for larger subtrees (measured: csg32 6.54 ms
-     * testing subtrees of >= 8 leaves vs 6.94 ms testing every BOUND record; with
-     * the later kernel 5.17 ms at >= 8, 5.11 at >= 6, 5.13 at >= 5, 5.30 at >= 12; with fused slab
-     * faces 4.93 at >= 6, 4.95 at 4 / 5, 4.98 at 7, 4.99 at 8; csg256 balanced 15.0 at 6, 15.2 at 4 / 8).
-     * Round 2, with the union count (csg32 now takes the spatial collect): csg256 balanced
-     * 10.02 / 10.02 at 6, 9.84 / 9.80 at 4, 9.82 at 3, 10.00 at 5, 10.46 at 8. */
+    /* Wave-level BOUND tests pay only for larger subtrees (csg32 5.17 ms testing
+     * subtrees of >= 8 leaves vs 6.94 testing every BOUND; later 4.93 at >= 6, 4.95
+     * at 4 / 5; csg256 balanced with the union count 9.80 at 4, 10.02 at 6, 10.46 at 8). */
     g.bound_min_leaves = 4;
-    {
-        const char* v = getenv("WOLOLO_JIT_BOUND_MIN_LEAVES");
-        if (v && *v) g.bound_min_leaves = (uint32_t)strtoul(v, NULL, 10);
-    }
     /* Event window: the LDS list wins where rays meet few events per trace and
      * the register window where they meet many (a deep difference chain carves
      * every sphere the ray passes).  Measured, 1920x1080x64: csg32 6.40 vs 6.47 ms,
      * csg256 balanced 20.2 vs 21.4, csg256 chain 35.8 vs 33.9.  Tree depth
      * separates them. */
     g.lds_events = tree_depth(prog, n_recs) <= 32u;
-    {
-        const char* v = getenv("WOLOLO_JIT_LDS_EVENTS");
-        if (v && *v) g.lds_events = v[0] != '0';
-    }
-    /* LDS list behind two register slots (PairLdsWindow): slower (csg32 4.69 ->
-     * 4.92 ms, csg256 balanced 13.99 -> 14.75): the two u64 slots spill at the
-     * 64-VGPR budget */
-    g.pair_window = 0;
-    {
-        const char* v = getenv("WOLOLO_JIT_PAIR_WINDOW");
-        if (v && *v) g.pair_window = v[0] != '0';
-    }
-    /* constants as VALU literals (csg32 4.46 -> 4.38 ms, csg256 balanced 13.48 ->
-     * 13.01, chain 26.27 -> 25.27 for the spheres alone) */
-    g.lit_consts = 1;
-    {
-        const char* v = getenv("WOLOLO_JIT_LIT_CONSTS");
-        if (v && *v) g.lit_consts = v[0] != '0';
-    }
-    g.fused_sphere = 1;
-    {
-        const char* v = getenv("WOLOLO_JIT_FUSED_SPHERE");
-        if (v && *v) g.fused_sphere = v[0] != '0';
-    }
     g.first_event = n_prims <= 64u * 32u;
-    {
-        const char* v = getenv("WOLOLO_JIT_FIRST_EVENT");
-        if (v && *v) g.first_event = v[0] != '0' && g.first_event;
-    }
-    g.axis_pairs = 1;
-    {
-        const char* v = getenv("WOLOLO_JIT_AXIS_PAIRS");
-        if (v && *v) g.axis_pairs = v[0] != '0';
-    }
-    g.member_skip = 1;
-    {
-        const char* v = getenv("WOLOLO_JIT_MEMBER_SKIP");
-        if (v && *v) g.member_skip = v[0] != '0';
-    }
-    g.flat_eval = 1;
-    {
-        const char* v = getenv("WOLOLO_JIT_FLAT_EVAL");
-        if (v && *v) g.flat_eval = v[0] != '0';
-    }
-    /* incremental union count: 1 = when the root is a union of >= 8 literal-set terms (csg32: 9 terms, 3.73 -> 3.68 ms), 2 = whenever it is one */
-    g.union_count = 1;
-    {
-        const char* v = getenv("WOLOLO_JIT_UNION_COUNT");
-        if (v && *v) g.union_count = (int)strtol(v, NULL, 10);
-    }
-    g.dl_eval = 1;
-    {
-        const char* v = getenv("WOLOLO_JIT_DL_EVAL");
-        if (v && *v) g.dl_eval = v[0] != '0';
-    }
     uint32_t nbounds = 0;
-    /* with the member skip, a bound around one convex primitive costs more than it
-     * saves (csg32 4.87 / 4.87 ms with it, 4.83 / 4.82 without, same box) */
-    g.bound_single = 0;
-    {
-        const char* v = getenv("WOLOLO_JIT_BOUND_SINGLE");
-        if (v && *v) g.bound_single = v[0] != '0';
-    }
-    /* spatial collect (surface-area splits, leaves of <= 8): by default for deep
-     * trees (no union-cluster hierarchy to cull with: csg256 chain 18.40 -> 13.59 ms)
-     * and small scenes (csg32 3.716 -> 3.586 ms, 3840x2160x256 56.08 -> 54.45);
-     * csg256 balanced's SAH cluster hierarchy over its pairs culls better (10.10 vs
-     * 10.58 ms).  WOLOLO_JIT_SPATIAL=0|1 forces it either way. */
+    /* spatial collect (surface-area splits, leaves of <= 8): for deep trees (no
+     * union-cluster hierarchy to cull with: csg256 chain 18.40 -> 13.59 ms) and small
+     * scenes (csg32 3.716 -> 3.586 ms, 3840x2160x256 56.08 -> 54.45); csg256
+     * balanced's SAH cluster hierarchy over its pairs culls better (10.10 vs 10.58
+     * ms).  Leaves: median splits, chain 15.04 / 13.93 / 13.63 ms at 2 / 4 / 8; SAH,
+     * csg32 3.687 / 3.612 / 3.628 / 3.589 at 3 / 4 / 6 / 8. */
     g.spatial = !g.lds_events || n_prims <= 64u;
-    g.spatial_leaf = 8; /* median splits, chain: 15.04 / 13.93 / 13.63 ms at 2 / 4 / 8; SAH, csg32: 3.687 / 3.612 / 3.628 / 3.589 at 3 / 4 / 6 / 8 */
-    {
-        const char* v = getenv("WOLOLO_JIT_SPATIAL");
-        if (v && *v) g.spatial = v[0] != '0';
-        v = getenv("WOLOLO_JIT_SPATIAL_SAH");
-        g.spatial_sah = !(v && *v && v[0] == '0');
-        v = getenv("WOLOLO_JIT_SPATIAL_CT");
-        g.spatial_ct = v && *v ? strtod(v, NULL) : 0.0;
-        v = getenv("WOLOLO_JIT_SPATIAL_LEAF");
-        if (v && *v) g.spatial_leaf = (uint32_t)strtoul(v, NULL, 10);
-        v = getenv("WOLOLO_JIT_TERM_DIST");
-        g.term_dist = v && *v ? v[0] != '0' : 0;
-        v = getenv("WOLOLO_JIT_CULL_BARRIER");
-        /* default 2, re-collects only (1080p64: csg256 chain 13.51 -> 13.21 ms, balanced
-         * 9.70 -> 9.47, csg32 3.273 -> 3.238; the sweep step's barrier as well, 1: 13.29 /
-         * 9.50 / 3.238), except for a general root evaluation over the LDS event list
-         * (csg32_nested 10.92 -> 11.75: its SGPR spills became 564 spilled VGPRs);
-         * the LDS-list case is settled below, where the root's form is known */
-        g.cull_barrier = v && *v ? (int)strtol(v, NULL, 10) : -1;
-        v = getenv("WOLOLO_JIT_KEY_VMOV");
-        g.key_vmov = v && *v ? v[0] != '0' : 0;
-        v = getenv("WOLOLO_JIT_DIST_CULL");
-        g.dist_cull = v && *v ? v[0] != '0' : 0;
-        if (g.spatial_leaf < 1u) g.spatial_leaf = 1u;
-    }
+    g.spatial_leaf = 8;
     /* term mode: where the root allows it, the tree is shallow enough for the
      * event-list path it replaces, and the scene is small enough for the spatial
      * groups over terms to cull as well as the scene compiler's cluster hierarchy
      * (<= 64 primitives: csg32 3.59 -> 3.33 ms; csg256 balanced 9.83 -> 12.40, so off
-     * there).  WOLOLO_JIT_TERMS=0|1 forces it either way. */
+     * there). */
     uint32_t n_jterms = 0;
     JTerm* jterms = NULL;
-    {
-        const char* v = getenv("WOLOLO_JIT_TERMS");
-        const int want = v && *v ? v[0] != '0' : n_prims <= 64u;
-        if (want && g.lds_events && n_prims) jterms = jit_terms(prog, n_recs, n_prims, &n_jterms);
-    }
+    if (n_prims <= 64u && g.lds_events && n_prims) jterms = jit_terms(prog, n_recs, n_prims, &n_jterms);
     SPrim* tunb = NULL;
     if (jterms) {
         uint32_t* pc_of = (uint32_t*)malloc(sizeof(uint32_t) * n_prims);
@@ -1724,67 +1446,6 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             if (prim_sphere(prog, pc, &sprims[g.nsprims])) ++g.nsprims;
             pc += 1u + prog[pc].u0;
         }
-        /* WOLOLO_JIT_SPATIAL_UNITS=1: when the root is a union of literal-set terms, a
-         * term's primitives stay together as one unit of the hierarchy, bounded as the
-         * term's value is: a conjunction lies inside each of its positive literals (the
-         * smallest one's sphere: a pair a - b is bounded by a, and b is skipped with it,
-         * which is exact -- b only matters inside a), a disjunction inside the sphere
-         * around all of its primitives */
-        const char* uv = getenv("WOLOLO_JIT_SPATIAL_UNITS");
-        if (sprims && uv && uv[0] == '1' && n_prims) {
-            UTerm* ut = (UTerm*)malloc(sizeof(UTerm) * n_prims);
-            uint32_t* pc_of = (uint32_t*)malloc(sizeof(uint32_t) * n_prims);
-            const uint32_t nt = ut && pc_of ? union_terms(prog, n_recs, n_prims, ut, n_prims) : 0u;
-            if (nt && pc_of) {
-                for (uint32_t pc = 0; pc < n_recs;) {
-                    if (prog[pc].op != WO_OP_PRIM) {
-                        ++pc;
-                        continue;
-                    }
-                    pc_of[prog[pc].u1] = pc;
-                    pc += 1u + prog[pc].u0;
-                }
-                for (uint32_t i = 0; i < nt; ++i) {
-                    if (__builtin_popcountll(ut[i].m) < 2 || __builtin_popcountll(ut[i].m) > SUNIT_MAX) continue;
-                    SPrim u, parts[SUNIT_MAX], pos;
-                    memset(&pos, 0, sizeof pos);
-                    memset(&u, 0, sizeof u);
-                    int ok = 1, have_pos = 0;
-                    for (uint32_t bit = 0; bit < 64u && ok; ++bit) {
-                        if (!((ut[i].m >> bit) & 1u)) continue;
-                        const uint32_t o = 32u * ut[i].w + bit;
-                        ok = o < n_prims;
-                        if (!ok) break;
-                        const uint32_t pc = pc_of[o];
-                        const int bnd = prim_sphere(prog, pc, &parts[u.npc]);
-                        if (!ut[i].neg && ((ut[i].q >> bit) & 1u)) { /* a positive literal of a conjunction */
-                            if (bnd && (!have_pos || parts[u.npc].r < pos.r)) pos = parts[u.npc], have_pos = 1;
-                        } else if (ut[i].neg) {
-                            ok = bnd; /* a disjunction needs every member bounded */
-                        }
-                        u.pcs[u.npc++] = pc;
-                    }
-                    if (!ok || (!ut[i].neg && !have_pos)) continue; /* stays as single primitives */
-                    if (ut[i].neg) {
-                        sprim_bound(parts, u.npc, u.c, &u.r);
-                    } else {
-                        u.c[0] = pos.c[0], u.c[1] = pos.c[1], u.c[2] = pos.c[2], u.r = pos.r;
-                    }
-                    u.pc = u.pcs[0];
-                    /* the unit replaces its primitives (bounded ones in the single list, the
-                     * unbounded ones in the ungrouped list: gen_collect_spatial checks units) */
-                    for (uint32_t k = 0; k < u.npc; ++k)
-                        for (uint32_t j = 0; j < g.nsprims; ++j)
-                            if (!sprims[j].npc && sprims[j].pc == u.pcs[k]) {
-                                sprims[j] = sprims[--g.nsprims];
-                                break;
-                            }
-                    sprims[g.nsprims++] = u;
-                }
-            }
-            free(ut);
-            free(pc_of);
-        }
         /* outsized primitives (radius > 16x the median, e.g. a ground sphere) stay
          * out of the hierarchy, as the scene compiler keeps them out of its BVHs:
          * inside it they would make every group above them a sphere no ray misses */
@@ -1833,26 +1494,29 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     for (uint32_t i = 0; i < n_recs; ++i)
         if ((prog[i].op == WO_LEAF_SPHERE || prog[i].op == WO_LEAF_HALFSPACE) && prog[i].u0 + 1u > n_mats_used)
             n_mats_used = prog[i].u0 + 1u;
-    int lds_prog = (size_t)n_recs * sizeof(WoRec) + (size_t)n_mats_used * sizeof(WoMaterial) + 4u * n_prims <= 6144u;
-    {
-        const char* v = getenv("WOLOLO_JIT_LDS_PROG");
-        if (v && *v) lds_prog = v[0] != '0';
-    }
+    const int lds_prog =
+        (size_t)n_recs * sizeof(WoRec) + (size_t)n_mats_used * sizeof(WoMaterial) + 4u * n_prims <= 6144u;
     /* the incremental union count's term table, per primitive: its term's mask test */
     uint32_t n_uterms = 0, eval_ops = 0;
     UTerm* uterms = NULL;
-    if (g.union_count && n_prims && !g.term_mode) {
+    /* when the root is a union of >= 8 literal-set terms (csg32: 9 terms, 3.73 ->
+     * 3.68 ms before term mode took it; csg256 balanced's 65) */
+    if (n_prims && !g.term_mode) {
         uterms = (UTerm*)malloc(sizeof(UTerm) * n_prims);
         if (!uterms) g.err = 1;
         else n_uterms = union_terms(prog, n_recs, n_prims, uterms, n_prims);
-        if (n_uterms < (g.union_count >= 2 ? 1u : 8u)) n_uterms = 0;
+        if (n_uterms < 8u) n_uterms = 0;
     }
     /* A full LDS event list keeps its smallest keys (WO_LDS_KEEP_SMALLEST): csg32_nested
      * 20.18 -> 10.97 ms (re-collects per segment 0.86 -> 0.18).  A union of small
      * terms (csg32, csg256 balanced) rarely fills the list, and there the eviction
      * code costs csg32 3.608 -> 3.701 ms: off for the union count. */
     if (g.lds_events && n_uterms) bput(&b, "#ifndef WO_LDS_KEEP_SMALLEST\n#define WO_LDS_KEEP_SMALLEST 0\n#endif\n");
-    if (g.cull_barrier < 0) g.cull_barrier = g.lds_events && !n_uterms && !g.term_mode ? 0 : 2;
+    /* the cull words through an opaque move in re-collects (csg256 chain 13.51 ->
+     * 13.21 ms, balanced 9.70 -> 9.47, csg32 3.273 -> 3.238), except for a general
+     * root evaluation over the LDS event list (csg32_nested 10.92 -> 11.75: its SGPR
+     * spills became 564 spilled VGPRs) */
+    g.cull_barrier = !(g.lds_events && !n_uterms && !g.term_mode);
     /* the register window for deep trees holds 5 events (csg256 chain 29.5 ms at 4,
      * 27.6 at 6, 27.5 at 8; with decision lists 19.36 at 4, 18.47 at 5, 18.65 at 6) */
     if (!g.lds_events) bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW 5\n#endif\n");
@@ -1863,7 +1527,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     if (g.lds_events && n_prims <= 64u) bput(&b, "#ifndef WO_LDS_EVENTS\n#define WO_LDS_EVENTS 7\n#endif\n");
     /* a general root evaluation sweeps many events per segment (csg32_nested
      * 4.5): its LDS list is sorted once per collect (SortedLdsWindow) */
-    const int sorted_win = g.lds_events && !g.pair_window && !n_uterms && !g.term_mode;
+    const int sorted_win = g.lds_events && !n_uterms && !g.term_mode;
     bput(&b, "#ifndef WO_SORTED_EVENTS\n#define WO_SORTED_EVENTS %d\n#endif\n", sorted_win);
     bput(&b, "#include \"wo_device_common.h\"\n"
              "#if WO_SORTED_EVENTS\n#define WO_SORTED_WINDOW wodev::SortedLdsWindow\n"
@@ -1888,19 +1552,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  (unsigned long long)u->q, u->w, u->neg);
         }
         bput(&b, "};\n");
-        /* the table in LDS (WOLOLO_JIT_LDS_UTERM=1): no gain for csg32 (3.614 / 3.583 ms
-         * against 3.581 / 3.597 from constant memory), csg256 balanced 10.01 -> 11.57 (LDS
-         * occupancy); off */
-        int lds_ut = 0;
-        {
-            const char* v = getenv("WOLOLO_JIT_LDS_UTERM");
-            if (v && *v) lds_ut = v[0] != '0';
-        }
-        if (lds_ut)
-            bput(&b, "__shared__ WoUTerm s_uterm[%u];\n#define WO_UTERM s_uterm\n#define WO_JIT_LDS_UTERM %u\n", n_prims,
-                 n_prims * 8u);
-        else
-            bput(&b, "#define WO_UTERM kUTerm\n");
+        /* (the table in LDS: no gain for csg32, csg256 balanced 10.01 -> 11.57 ms from
+         * the LDS occupancy) */
+        bput(&b, "#define WO_UTERM kUTerm\n");
     }
     bput(&b, "__constant__ uint32_t kOrdPc[%u] = {", n_prims ? n_prims : 1u);
     if (!n_prims) bput(&b, "0u");
@@ -1985,11 +1639,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "    uint64_t after = 0ull, key = 0ull;\n"
              "    WO_MARK(\"collect_begin\");\n"
              "    {\n",
-             !g.lds_events ? "wodev::Window"
-             : g.pair_window ? "wodev::PairLdsWindow"
-             : sorted_win    ? "WO_SORTED_WINDOW"
-                             : "wodev::LdsWindow",
-             !g.lds_events ? "" : g.pair_window ? "win.rest.ev = ev; " : "win.ev = ev; ");
+             !g.lds_events ? "wodev::Window" : sorted_win ? "WO_SORTED_WINDOW" : "wodev::LdsWindow",
+             !g.lds_events ? "" : "win.ev = ev; ");
         g.first_pass = 1;
         gen_collect_all(&g, 6);
         bput(&b,
@@ -2037,21 +1688,17 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             bput(&b,
                  "    for (;;) {\n"
                  "      uint32_t r;\n");
-            if (g.cull_barrier == 1) gen_cull_barrier(&g, 6);
             bput(&b,
                  "      // WO_EVAL_BEGIN (the root's value from bits[] and cull[]; tests/test_jit.py compiles it on the host)\n"
                  "      {\n");
             g.nbound = 0;
-            if (g.flat_eval) {
+            {
                 Term rt = gen_eval_flat(&g, 0, n_recs, 8);
                 const uint32_t m = rt.kind ? (rt.P | rt.N) : 0u;
                 eval_ops = rt.dl && dl_cost(&g, rt.dl) < rt.cost + (m ? 3u : 0u) ? dl_cost(&g, rt.dl)
                                                                                  : rt.cost + (m ? 3u : 0u);
                 uint32_t rv = term_name(&g, &rt, 8);
                 bput(&b, "        r = v%u ? 1u : 0u;\n      }\n", rv);
-            } else {
-                uint32_t rv = gen_eval(&g, 0, n_recs, 8);
-                bput(&b, "        r = v%u;\n      }\n", rv);
             }
             bput(&b, "      // WO_EVAL_END\n");
             bput(&b,
@@ -2123,16 +1770,7 @@ kernel_tail:
          "  tr.ordpc = kOrdPc;\n"
          "  const WoMaterial* m = mats;\n"
          "#endif\n"
-         "#ifdef WO_JIT_LDS_UTERM  // the union count's term table (pathtrace_block's first barrier orders the copy)\n"
-         "  for (uint32_t i = threadIdx.x; i < WO_JIT_LDS_UTERM; i += wodev::kBlock)\n"
-         "    reinterpret_cast<uint32_t*>(s_uterm)[i] = reinterpret_cast<const uint32_t*>(kUTerm)[i];\n"
-         "#endif\n"
-         "#if WO_JIT_LDS_EVENTS && WO_SORT_RAYS\n"
-         "  static_assert(wodev::kLdsEvents >= 6u, \"a ray's state fits the event list column\");\n"
-         "  wodev::pathtrace_block<JitTracer, true>(tr, m, fr, local_rows, out, seg_slots, tg, s_ev);\n"
-         "#else\n"
          "  wodev::pathtrace_block(tr, m, fr, local_rows, out, seg_slots, tg);\n"
-         "#endif\n"
          "}\n",
          n_recs ? n_recs : 1u, n_mats_used, n_prims ? n_prims : 1u, n_recs * 8u, n_mats_used * 8u, n_prims);
     /* the root evaluation's operation count per swept event, for bench.py's

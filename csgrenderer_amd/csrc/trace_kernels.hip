@@ -298,11 +298,6 @@ struct InterpTracer {
 // last processed event, exactly as an overflowing window does.  Results are
 // the general algorithm's, bit for bit.
 // ---------------------------------------------------------------------------
-// Compact traversal node: geo = BOUND (centre, R) or sphere primitive (centre,
-// r^2); aux = kind << 30 | value (BOUND: skip target, primitives: ordinal).
-// Generic primitives (half-spaces, several members) read their leaves from the
-// program.  20 bytes per node, staged in LDS when the table fits.
-constexpr uint32_t kNodeBound = 0u, kNodeSphere = 1u, kNodeGeneric = 2u;
 
 // Ordered BVH traversal (the common case).  The host builds a binary AABB
 // hierarchy over the bounded primitives (build_lbvh; each node holds its two
@@ -328,10 +323,6 @@ constexpr uint32_t kTermRecF4 = 5, kTermLitSphere = 1, kTermLitSphere2 = 2;  // 
 // and the per-lane LDS stack holds as many entries as the built tree has levels:
 // a walk pushes at most one sibling per ancestor, so the stack never overflows.
 constexpr uint32_t kLaneDepthMax = 24;
-#ifndef WO_LANES_WIDE_DEFAULT
-#define WO_LANES_WIDE_DEFAULT 0
-#endif
-constexpr bool kLanesWideDefault = WO_LANES_WIDE_DEFAULT != 0;  // WOLOLO_LANES_WIDE overrides
 #ifndef WO_LANES_TERM2
 #define WO_LANES_TERM2 1  // term visits of two spheres in all: two sphere tests (visit_leaf)
 #endif
@@ -344,14 +335,6 @@ constexpr bool kLanesWideDefault = WO_LANES_WIDE_DEFAULT != 0;  // WOLOLO_LANES_
 #ifndef WO_LANES_PRIO_TERM
 #define WO_LANES_PRIO_TERM 0  // the same at a term record's load (term mode; csg512 44.93 -> 44.70 ms in an A/B, not yet verified on by default)
 #endif
-#ifndef WO_LANES_HALF_DEFAULT
-#define WO_LANES_HALF_DEFAULT 0
-#endif
-constexpr bool kLanesHalfDefault = WO_LANES_HALF_DEFAULT != 0;  // WOLOLO_LANES_HALF overrides
-#ifndef WO_LANES_DYN_DEFAULT
-#define WO_LANES_DYN_DEFAULT 0
-#endif
-constexpr bool kLanesDynDefault = WO_LANES_DYN_DEFAULT != 0;  // WOLOLO_LANES_DYN overrides
 #ifndef WO_LANES_FUSED_SPHERE
 #define WO_LANES_FUSED_SPHERE 1
 #endif
@@ -377,49 +360,32 @@ __device__ __forceinline__ float box_near(float4 lo, float4 hi, F3 ri, F3 oi, fl
 // The same over a child box stored as fp16 (lb_half: lo rounded down, hi up, so
 // the box only grows): q.x = lo.x | lo.y << 16, q.y = lo.z | hi.x << 16, q.z =
 // hi.y | hi.z << 16.  The conversions fold into v_fma_mix_f32.
-__device__ __forceinline__ float h16(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (unsigned short)u); }
-__device__ __forceinline__ float box_near_h(uint4 q, F3 ri, F3 oi, float& far_t) {
-    const float ax = __builtin_fmaf(h16(q.x & 0xffffu), ri.x, -oi.x), bx = __builtin_fmaf(h16(q.y >> 16), ri.x, -oi.x);
-    const float ay = __builtin_fmaf(h16(q.x >> 16), ri.y, -oi.y), by = __builtin_fmaf(h16(q.z & 0xffffu), ri.y, -oi.y);
-    const float az = __builtin_fmaf(h16(q.y & 0xffffu), ri.z, -oi.z), bz = __builtin_fmaf(h16(q.z >> 16), ri.z, -oi.z);
-    const float n = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-    far_t = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-    return n;
-}
-
-// kMode: 0 general walk over the table in LDS, 1 general walk over the table in
-// global memory, 2 ordered BVH, 3 ordered BVH over single-sphere primitives only
-// (no generic-primitive code: fewer registers); 4 / 5 = 2 / 3 with 16-bit stack
-// entries (trees of < 2^15 nodes and primitives: half the stacks' LDS, left to
-// top nodes); 6 ordered BVH over the terms of a root that is a union of small
-// conjunctions (extract_terms: the leaves and the always list hold terms);
-// 7 / 8 / 9 = 3 / 2 / 6 over a 4-wide tree (lb_collapse4: four child boxes per
-// node, half the dependent node loads of a walk), always with 16-bit stacks.
-// 11 / 12 / 13 / 14 = 3 / 2 / 6 / 9 with the resumable walk (trace_step, dynamic ray fetch);
-// 15 = 3 over nodes of fp16 child boxes (half the bytes: twice the nodes in LDS).
+// kMode (PathKind): 2 ordered BVH over union-only primitives, 3 the same over
+// single-sphere primitives only (no generic-primitive code: fewer registers),
+// 6 ordered BVH over the terms of a root that is a union of small conjunctions
+// (extract_terms: the leaves and the always list hold terms), 14 term mode over a
+// 4-wide tree (lb_collapse4: four child boxes per node, half the dependent node
+// loads of a walk; 16-bit stacks) with the resumable walk (trace_step, dynamic
+// ray fetch).  Measured and removed: the general BOUND walk,
+// 16-bit stacks for binary trees, 4-wide trees for primitives, resumable binary
+// walks, a uniform grid and fp16 child boxes.
 template <int kModeT, bool kCountT>
 struct LaneTracer {
+    static_assert(kModeT == 2 || kModeT == 3 || kModeT == 6 || kModeT == 14, "lane tracer forms");
     static constexpr bool kCount = kCountT;
-    static constexpr bool kDyn = kModeT >= 11 && kModeT <= 14;
+    static constexpr bool kDyn = kModeT == 14;
     static constexpr bool kResumable = kDyn;
-    static constexpr bool kHalf = kModeT == 15;  // binary nodes with fp16 child boxes (lb_half)
-    static constexpr int kMode = kModeT == 11 ? 3 : kModeT == 12 ? 2 : kModeT == 13 ? 6 : kModeT == 14 ? 9
-                               : kModeT == 15 ? 3 : kModeT;
-    static constexpr bool kBvh = kMode >= 2;
-    static constexpr bool kWide = kMode >= 7 && kMode <= 9;
-    static constexpr bool kGrid = kMode == 10;
-    static constexpr bool kSpheresOnly = kMode == 3 || kMode == 5 || kMode == 7 || kMode == 10;
-    static constexpr bool kStack16 = kMode == 4 || kMode == 5 || kWide;
-    static constexpr bool kTerms = kMode == 6 || kMode == 9;
-    static constexpr uint32_t kNodeF4 = kWide ? 7u : (kHalf ? 2u : 4u);  // float4 per node
+    static constexpr int kMode = kModeT;
+    static constexpr bool kWide = kMode == 14;
+    static constexpr bool kSpheresOnly = kMode == 3;
+    static constexpr bool kStack16 = kWide;
+    static constexpr bool kTerms = kMode == 6 || kMode == 14;
+    static constexpr uint32_t kNodeF4 = kWide ? 7u : 4u;  // float4 per node
     WorkCounts wk;
     uint64_t tmark;  // section timing (counting builds)
     const WoRec* __restrict__ prog;      // full program (generic primitives, hit leaves)
-    const float4* geo;                   // LDS or global
-    const uint32_t* aux;
     const uint32_t* __restrict__ ordpc;  // ordinal -> program pc
-    uint32_t ntrav;
-    // ordered BVH (build_lbvh); lroot == kNoRef and nalways == 0: general walk only
+    // ordered BVH (build_lbvh)
     const float4* __restrict__ lnodes;   // 4 float4 per node: childA lo|ref, childA hi|ref B, childB lo, childB hi
     const float4* __restrict__ lgeo;     // per ordinal: sphere centre, r^2 (single-sphere primitives)
     const uint32_t* __restrict__ lkind;  // per ordinal: 1 = single sphere, 0 = generic; then the always list
@@ -439,26 +405,14 @@ struct LaneTracer {
     typedef const float4* LdsNodes;
     typedef const float4* GlobalNodes;
 #endif
-#if defined(__HIP_DEVICE_COMPILE__)
-    typedef const __attribute__((address_space(3))) uint4* LdsNodesU4;
-    typedef const __attribute__((address_space(1))) uint4* GlobalNodesU4;
-#else
-    typedef const uint4* LdsNodesU4;
-    typedef const uint4* GlobalNodesU4;
-#endif
     LdsNodes ltop;
     uint32_t ntop;
-    // uniform grid (kMode 10, build_grid): cell c's ordinals are gitems[gcells[c] .. gcells[c + 1])
-    float glo[3], gh[3], ginv[3];
-    uint32_t gres[3];
-    const uint32_t* __restrict__ gcells;
-    const uint32_t* __restrict__ gitems;
 
     // single-sphere scenes: per ordinal its leaf record, then its material (LaneBvh::leaves)
     const WoRec* __restrict__ lleaf;
-    static constexpr bool kHitMaterial = kSpheresOnly && kBvh;
+    static constexpr bool kHitMaterial = kSpheresOnly;
     __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const {
-        if constexpr (kSpheresOnly && kBvh)
+        if constexpr (kSpheresOnly)
             return lleaf[2u * h.ord];  // one load (the record of the ordinal's only member)
         else
             return prog[ordpc[h.ord] + 1u + h.member];
@@ -468,7 +422,7 @@ struct LaneTracer {
         return reinterpret_cast<const WoMaterial*>(lleaf)[2u * h.ord + 1u];
     }
 
-    // Interval of primitive `ord` (the general walk's arithmetic, bit for bit).
+    // Interval of primitive `ord` (the interpreter's arithmetic, bit for bit).
     __device__ __forceinline__ Ivl prim_ivl(uint32_t ord, F3 o, F3 d, F3& inv, bool& have_inv) {
         Ivl iv;
         if (kSpheresOnly || lkind[ord] != 0u) {
@@ -507,66 +461,6 @@ struct LaneTracer {
         return iv;
     }
 
-    // Uniform-grid walk (3-D DDA, Amanatides & Woo): cells in ray order from the
-    // grid's entry (a re-query from the last key's t), each cell's primitives
-    // visited (a primitive spans several cells: the minimum is idempotent, and the
-    // count at t_min is taken in the first cell only, which holds every primitive
-    // containing the ray's start: build_grid bins each box grown by more than
-    // t_min).  The walk stops once the best key precedes the current cell's exit
-    // (less a margin for the DDA's rounding): every later cell, and every event in
-    // it, begins after that exit.  The cell sequence needs no loads, so the next
-    // cell's list is fetched while this one's spheres are tested.
-    template <class Visit>
-    __device__ __forceinline__ void grid_walk(F3 o, F3 d, F3 ri, F3 oi, uint64_t after, const uint64_t& best,
-                                              uint32_t& cnt, Visit& visit) {
-        const float ax0 = __builtin_fmaf(glo[0], ri.x, -oi.x), ax1 = __builtin_fmaf(glo[0] + gh[0] * (float)gres[0], ri.x, -oi.x);
-        const float ay0 = __builtin_fmaf(glo[1], ri.y, -oi.y), ay1 = __builtin_fmaf(glo[1] + gh[1] * (float)gres[1], ri.y, -oi.y);
-        const float az0 = __builtin_fmaf(glo[2], ri.z, -oi.z), az1 = __builtin_fmaf(glo[2] + gh[2] * (float)gres[2], ri.z, -oi.z);
-        const float tenter = fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1));
-        const float texit = fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1));
-        const float tafter = after == 0ull ? 0.0f : __uint_as_float((uint32_t)(after >> 32));
-        const float t0 = fmaxf(tenter, fmaxf(__builtin_fmaf(-2e-5f, tafter, tafter) - 1e-5f, 0.0f));
-        if (!(t0 <= texit)) return;
-        // the start cell (clamped: t0 may round a hair outside the grid)
-        int ix = (int)floorf(((o.x + t0 * d.x) - glo[0]) * ginv[0]);
-        int iy = (int)floorf(((o.y + t0 * d.y) - glo[1]) * ginv[1]);
-        int iz = (int)floorf(((o.z + t0 * d.z) - glo[2]) * ginv[2]);
-        ix = min(max(ix, 0), (int)gres[0] - 1);
-        iy = min(max(iy, 0), (int)gres[1] - 1);
-        iz = min(max(iz, 0), (int)gres[2] - 1);
-        // steps and per-cell t increments recomputed at use (registers: the walk runs
-        // inside the path loop at 8 waves per SIMD)
-        float tnx = __builtin_fmaf(glo[0] + gh[0] * (float)(ix + (d.x >= 0.0f)), ri.x, -oi.x);
-        float tny = __builtin_fmaf(glo[1] + gh[1] * (float)(iy + (d.y >= 0.0f)), ri.y, -oi.y);
-        float tnz = __builtin_fmaf(glo[2] + gh[2] * (float)(iz + (d.z >= 0.0f)), ri.z, -oi.z);
-        bool first = after == 0ull;
-        uint32_t unused = 0;
-        for (;;) {
-            WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);  // grid: cell trips per wave
-            WO_WK(WO_WORK_BOUND_TESTS);       // grid: cells visited
-            const uint32_t c = ((uint32_t)iz * gres[1] + (uint32_t)iy) * gres[0] + (uint32_t)ix;
-            const uint32_t b0 = gcells[c], b1 = gcells[c + 1u];
-            for (uint32_t k = b0; k < b1; ++k) visit(gitems[k], first ? cnt : unused);
-            first = false;
-            const float tc = fminf(fminf(tnx, tny), tnz);  // this cell's exit
-            const float tb = best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(best >> 32));
-            if (tb < __builtin_fmaf(-2e-5f, tc, tc) - 1e-5f) break;
-            if (tnx <= tny && tnx <= tnz) {
-                ix += d.x >= 0.0f ? 1 : -1;
-                tnx += gh[0] * fabsf(ri.x);
-                if ((uint32_t)ix >= gres[0]) break;
-            } else if (tny <= tnz) {
-                iy += d.y >= 0.0f ? 1 : -1;
-                tny += gh[1] * fabsf(ri.y);
-                if ((uint32_t)iy >= gres[1]) break;
-            } else {
-                iz += d.z >= 0.0f ? 1 : -1;
-                tnz += gh[2] * fabsf(ri.z);
-                if ((uint32_t)iz >= gres[2]) break;
-            }
-        }
-    }
-
     // One query's walk state (query / trace_step): the smallest event key > `after`
     // found so far, whether the count rises there (term mode), the node to visit
     // next and the lane stack's depth, the primitives (terms) holding t_min met so
@@ -578,7 +472,7 @@ struct LaneTracer {
         bool up;
     };
 
-    // A leaf of the walk (or of the always list / a grid cell): a primitive, or in
+    // A leaf of the walk (or of the always list): a primitive, or in
     // term mode a term.  Term mode: a term (a conjunction of one or two literals,
     // each a primitive or its complement) changes value only at an event of a
     // literal X, and then exactly when the other literal holds at that key; it
@@ -823,23 +717,7 @@ struct LaneTracer {
             WO_WK_N(WO_WORK_BOUND_TESTS, 2u);
             float na, nb, fa, fb;
             uint32_t ra, rb;
-            if constexpr (kHalf) {
-                // per child: lo.x | lo.y, lo.z | hi.x, hi.y | hi.z as fp16 pairs, then its ref;
-                // the fp16 operands go into v_fma_mix_f32 unconverted
-                uint4 qa, qb;
-                if (cur < ntop) {
-                    const LdsNodesU4 nd = (LdsNodesU4)ltop + 2u * cur;
-                    qa = nd[0], qb = nd[1];
-                    asm volatile("");
-                } else {
-                    const GlobalNodesU4 nd = (GlobalNodesU4)lnodes + 2u * cur;
-                    qa = nd[0], qb = nd[1];
-                }
-                na = box_near_h(qa, ri, oi, fa);
-                nb = box_near_h(qb, ri, oi, fb);
-                ra = qa.w;
-                rb = qb.w;
-            } else {
+            {
                 float4 a0, a1, b0, b1;
 #if WO_LANES_PRIO
                 __builtin_amdgcn_s_setprio(WO_LANES_PRIO);  // a wave about to issue its node load goes first
@@ -900,13 +778,6 @@ struct LaneTracer {
                                               F3& inv, bool& have_inv) {
         QState s;
         qbegin(s, after, o, d, inv, have_inv);
-        if constexpr (kGrid) {
-            auto visit = [&](uint32_t ord, uint32_t& cnt) { visit_leaf(ord, cnt, s, o, d, inv, have_inv); };
-            grid_walk(o, d, ri, oi, after, s.best, s.cnt, visit);
-            inside = s.cnt;
-            up = !(s.best & kKeyTypeBit);
-            return s.best;
-        }
         while (s.cur != kNoRef) trip(s, o, d, ri, oi, inv, have_inv);
         inside = s.cnt;
         if constexpr (kTerms)
@@ -1009,125 +880,7 @@ struct LaneTracer {
         }
     }
 
-    __device__ __forceinline__ bool trace(F3 o, F3 d, Hit& hit) {
-        if constexpr (kBvh)
-            return trace_ordered(o, d, hit);
-        else
-            return trace_general(o, d, hit);
-    }
-
-    __device__ __forceinline__ bool trace_general(F3 o, F3 d, Hit& hit) {
-        const float tmin = WO_T_MIN;
-        F3 inv = f3(0.0f, 0.0f, 0.0f);
-        bool have_inv = false;
-        Window win;
-        int cnt = 0;  // primitives containing the current point
-        uint32_t root = 0;
-        uint64_t after = 0ull, key = 0ull;
-        bool first = true;
-        for (;;) {
-            win.clear();
-            uint64_t kcut = kEmptyKey;
-            uint32_t pc = 0;
-            while (pc < ntrav) {
-                const uint32_t a = aux[pc];
-                const float4 g = geo[pc];
-                const uint32_t kind = a >> 30, val = a & 0x3fffffffu;
-                // BOUND and sphere nodes share the centre-to-line arithmetic, so lanes
-                // at different node kinds run it once: b = (o - c).d, ll = distance^2
-                // (a generic primitive's lanes compute it and ignore it)
-                float b, ll;
-                sphere_bl(g.x, g.y, g.z, o, d, b, ll);
-                if (kind == kNodeBound) {
-                    WO_WK(WO_WORK_BOUND_TESTS);
-                    // tca = (c - o).d = -b; ll is the same bits either way
-                    const float tca = -b, d2 = ll;
-                    bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, g.w * g.w)) || (tca + g.w < 0.0f);
-                    // near end of the sphere along the ray, rounded down generously
-                    float lo = (tca - g.w) - 1e-5f * (fabsf(tca) + g.w);
-                    // prune when every event of the subtree keys after the nearest
-                    // event so far (an empty window never prunes): the barrier then
-                    // lies strictly after that event, so each sweep makes progress
-                    const uint64_t kc = key_floor(lo);
-                    bool prune = !miss && lo > 0.0f && kc > win.k[0];
-                    if (prune) kcut = kc < kcut ? kc : kcut;
-                    pc = (miss || prune) ? val : pc + 1u;
-                } else {
-                    Ivl iv;
-                    if (kind == kNodeSphere) {
-                        WO_WK(WO_WORK_SPHERE_TESTS);
-                        float la, lb;
-                        sphere_interval_bl(b, ll, g.w, la, lb);
-                        ivl_first(iv, la, lb);
-                    } else {
-                        const uint32_t ppc = ordpc[val];
-                        const uint32_t count = prog[ppc].u0;
-                        for (uint32_t m = 0; m < count; ++m) {
-                            WoRec L = prog[ppc + 1u + m];
-                            float la, lb;
-                            WO_WK(L.op == WO_LEAF_SPHERE ? WO_WORK_SPHERE_TESTS : WO_WORK_HALFSPACE_TESTS);
-                            if (L.op == WO_LEAF_SPHERE) {
-                                sphere_interval(L.f[0], L.f[1], L.f[2], L.f[3], o, d, la, lb);
-                            } else if (L.u1 != 0u) {
-                                if (!have_inv) {
-                                    inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-                                    have_inv = true;
-                                }
-                                uint32_t ax = L.u1 - 1u;
-                                halfspace_axis_interval(ax == 0u ? L.f[0] : (ax == 1u ? L.f[1] : L.f[2]), L.f[3],
-                                                        pick3(o, ax), pick3(d, ax), pick3(inv, ax), la, lb);
-                            } else {
-                                halfspace_interval(L.f[0], L.f[1], L.f[2], L.f[3], o, d, la, lb);
-                            }
-                            if (m == 0u)
-                                ivl_first(iv, la, lb);
-                            else
-                                ivl_meet(iv, la, lb, m);
-                        }
-                    }
-                    if (!(iv.a > iv.b)) {
-                        if (first && iv.a <= tmin && iv.b > tmin) ++cnt;
-                        uint64_t k0 = event_key(iv.a, val, 0u, iv.ma), k1 = event_key(iv.b, val, 1u, iv.mb);
-                        if (iv.a > tmin && k0 > after) {
-                            WO_WK(WO_WORK_EVENTS);
-                            win.insert(k0);
-                        }
-                        if (iv.b > tmin && iv.b < kInf && k1 > after) {
-                            WO_WK(WO_WORK_EVENTS);
-                            win.insert(k1);
-                        }
-                    }
-                    ++pc;
-                }
-            }
-            if (first) {
-                first = false;
-                if (win.k[0] == kEmptyKey) return false;
-                root = cnt > 0 ? 1u : 0u;
-            }
-            // sweep up to the barrier
-            bool again = false;
-            for (;;) {
-                uint64_t nk = win.k[0];
-                if (nk == kEmptyKey || nk >= kcut) {
-                    again = win.dropped() || kcut != kEmptyKey;
-                    break;
-                }
-                key = win.pop();
-                WO_WK(WO_WORK_SWEEP_STEPS);
-                cnt += (key & kKeyTypeBit) ? -1 : 1;
-                uint32_t rv = cnt > 0 ? 1u : 0u;
-                if (rv != root) {
-                    hit_from_key(key, rv, hit);
-                    return true;
-                }
-                root = rv;
-            }
-            if (!again) return false;
-            WO_WK(WO_WORK_RECOLLECTS);
-            after = key;
-        }
-    }
+    __device__ __forceinline__ bool trace(F3 o, F3 d, Hit& hit) { return trace_ordered(o, d, hit); }
 };
 
 #ifndef WO_LANES_MIN_WAVES
@@ -1143,15 +896,10 @@ struct LaneBvh {
     uint32_t nalways, root, nprims;
     uint32_t depth;        // internal levels of the tree: the lane stack's entries
     uint32_t ntop;         // nodes [0, ntop) staged in LDS after the lane stacks
-    uint32_t dyn_walkers;  // resumable walk: walking lanes at which a wave bails out (WOLOLO_LANES_DYN_WALKERS)
-    float glo[3], gh[3], ginv[3];  // uniform grid (kMode 10): origin, cell size, 1 / cell size
-    uint32_t gres[3];
-    const uint32_t* gcells;        // ncells + 1 offsets into gitems
-    const uint32_t* gitems;        // ordinals
+    uint32_t dyn_walkers;  // resumable walk: walking lanes at which a wave bails out
 };
 
-// Dynamic LDS: the BVH walk's lane stacks ([depth][kBlock] u32) and top nodes,
-// or (kLds) the general walk's table.
+// Dynamic LDS: the BVH walk's lane stacks ([depth][kBlock] u32 or u16) and top nodes.
 #ifndef WO_LANES_BVH_MIN_WAVES
 #define WO_LANES_BVH_MIN_WAVES 7  // rtiow_cover: 16.86 ms at 8, 16.63 at 7, 17.26 at 6
 #endif
@@ -1165,39 +913,26 @@ template <int kMode, bool kCount>
 #ifndef WO_LANES_DYN_TERMS_MIN_WAVES
 #define WO_LANES_DYN_TERMS_MIN_WAVES 6  // csg512_balanced: 56.4 ms at 6 (no spill), 57.2 at 7 (31 VGPRs spilled)
 #endif
-__global__ __launch_bounds__(kBlock, (kMode == 13 || kMode == 14) ? WO_LANES_DYN_TERMS_MIN_WAVES
-                                    : kMode >= 11 ? WO_LANES_DYN_MIN_WAVES
-                                    : (kMode == 6 || kMode == 9) ? WO_LANES_TERMS_MIN_WAVES
-                                    : (kMode == 2 || kMode == 4 || kMode == 7 || kMode == 8) ? WO_LANES_BVH_MIN_WAVES
-                                                                               : WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
-    const WoRec* __restrict__ prog, const float4* __restrict__ gnodes, const uint32_t* __restrict__ ordpc,
-    const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t ntrav, uint32_t local_rows, float4* __restrict__ out,
-    unsigned long long* __restrict__ seg_slots, PathLaunch tg, LaneBvh bvh) {
+__global__ __launch_bounds__(kBlock, kMode == 14  ? WO_LANES_DYN_TERMS_MIN_WAVES
+                                    : kMode == 6 ? WO_LANES_TERMS_MIN_WAVES
+                                    : kMode == 2 ? WO_LANES_BVH_MIN_WAVES
+                                                 : WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
+    const WoRec* __restrict__ prog, const uint32_t* __restrict__ ordpc, const WoMaterial* __restrict__ mats, WoFrame fr,
+    uint32_t local_rows, float4* __restrict__ out, unsigned long long* __restrict__ seg_slots, PathLaunch tg,
+    LaneBvh bvh) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    constexpr int kBase = LaneTracer<kMode, kCount>::kMode;  // the walk's form (11 / 12 / 13: resumable 3 / 2 / 6)
-    constexpr bool kLds = kBase == 0;
     LaneTracer<kMode, kCount> tr;
     tr.prog = prog;
     tr.ordpc = ordpc;
-    tr.ntrav = ntrav;
     tr.lnodes = bvh.nodes;
     tr.lgeo = bvh.geo;
     tr.lkind = bvh.kind;
     tr.ltrec = bvh.trec;
     tr.lleaf = bvh.leaves;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        tr.glo[a] = bvh.glo[a];
-        tr.gh[a] = bvh.gh[a];
-        tr.ginv[a] = bvh.ginv[a];
-        tr.gres[a] = bvh.gres[a];
-    }
-    tr.gcells = bvh.gcells;
-    tr.gitems = bvh.gitems;
     tr.nalways = bvh.nalways;
     tr.lroot = bvh.root;
     tr.nprims = bvh.nprims;
-    tr.stk = smem + threadIdx.x;  // kBase >= 2 only
+    tr.stk = smem + threadIdx.x;
     tr.stk16 = reinterpret_cast<uint16_t*>(smem) + threadIdx.x;
     tr.ntop = 0;
     tr.ltop = (typename LaneTracer<kMode, kCount>::LdsNodes)nullptr;
@@ -1205,7 +940,7 @@ __global__ __launch_bounds__(kBlock, (kMode == 13 || kMode == 14) ? WO_LANES_DYN
         tr.dpending = false;
         tr.dyn_walkers = bvh.dyn_walkers;
     }
-    if constexpr (kBase >= 2) {
+    {
         // the top levels of the BVH next to the stacks; pathtrace_block's first
         // barrier orders the copy before any walk
         constexpr bool kStack16 = LaneTracer<kMode, kCount>::kStack16;
@@ -1215,22 +950,6 @@ __global__ __launch_bounds__(kBlock, (kMode == 13 || kMode == 14) ? WO_LANES_DYN
         for (uint32_t i = threadIdx.x; i < kNodeF4 * bvh.ntop; i += kBlock) top[i] = bvh.nodes[i];
         tr.ltop = (typename LaneTracer<kMode, kCount>::LdsNodes)top;
         tr.ntop = bvh.ntop;
-    }
-    const uint32_t* gaux = reinterpret_cast<const uint32_t*>(gnodes + ntrav);
-    if constexpr (kLds) {
-        uint32_t* table = smem;
-        float4* lgeo = reinterpret_cast<float4*>(table);
-        uint32_t* laux = table + ntrav * 4u;
-        for (uint32_t i = threadIdx.x; i < ntrav; i += kBlock) {
-            lgeo[i] = gnodes[i];
-            laux[i] = gaux[i];
-        }
-        __syncthreads();
-        tr.geo = lgeo;
-        tr.aux = laux;
-    } else {
-        tr.geo = gnodes;
-        tr.aux = gaux;
     }
     pathtrace_block(tr, mats, fr, local_rows, out, seg_slots, tg);
 }
@@ -1485,31 +1204,21 @@ struct WoDev {
     float4* d_frame;
     size_t frame_cap;
     hipStream_t stream;
-    // lane traversal (union-only programs): compact nodes [geo float4 x n][aux u32 x n] + ordinal -> pc
-    float4* d_trav;
-    size_t trav_cap;
+    // lane tracer: ordinal -> program pc (generic primitives, hit leaves)
     uint32_t* d_ordpc;
     size_t ordpc_cap;
-    uint32_t n_trav;
     // the lane tracer's ordered BVH (build_lbvh): [4 float4 per node][float4 per
     // ordinal] then u32 [kind per ordinal][always list]
     float4* d_lbvh;
     size_t lbvh_cap;
     uint32_t lb_nodes, lb_always, lb_root, lb_nprims;
-    bool lb_spheres_only;  // every primitive is a single sphere (kMode 3 / 5)
-    bool lb_stack16;       // nodes and primitives < 2^15: 16-bit stack entries (kMode 4 / 5, 7 / 8 / 9)
-    bool lb_wide;          // 4-wide nodes of 7 float4 (lb_collapse4; kMode 7 / 8 / 9)
-    bool lb_grid;          // uniform grid over single spheres (build_grid; kMode 10)
-    float g_lo[3], g_h[3];
-    uint32_t g_res[3];
-    uint32_t* d_grid;      // [ncells + 1 offsets][items]
-    size_t grid_cap;
-    uint32_t g_items_off;
-    uint32_t lb_terms;     // term mode (kMode 6): terms the BVH's leaves and always list refer to
+    bool lb_spheres_only;  // every primitive is a single sphere (kind 3)
+    bool lb_stack16;       // 16-bit stack entries (the 4-wide tree)
+    bool lb_wide;          // 4-wide nodes of 7 float4 (lb_collapse4; kind 14)
+    uint32_t lb_terms;     // term mode (kinds 6 / 14): terms the BVH's leaves and always list refer to
     uint32_t last_kind;    // the PathKind of the last path launch (wo_dev_lanes_info)
     uint32_t lb_term_off;  // their records (kTermRecF4 float4 each) at this u32 offset of d_lbvh
     uint32_t lb_leaf_off;  // single-sphere scenes: per ordinal its leaf record (WoRec) at this u32 offset, else 0
-    bool lb_half;          // binary nodes of fp16 child boxes (2 float4 per node; kind 15)
     uint32_t lb_top;       // nodes staged in LDS per workgroup
     uint32_t lb_depth;     // internal levels of the lane BVH (<= kLaneDepthMax)
     unsigned long long* d_segslots;  // kSegSlots segment counters, kSegStride apart
@@ -1647,9 +1356,7 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
     if (dev->d_prog) (void)hipFree(dev->d_prog);
     if (dev->d_mats) (void)hipFree(dev->d_mats);
     if (dev->d_frame) (void)hipFree(dev->d_frame);
-    if (dev->d_trav) (void)hipFree(dev->d_trav);
     if (dev->d_lbvh) (void)hipFree(dev->d_lbvh);
-    if (dev->d_grid) (void)hipFree(dev->d_grid);
     if (dev->d_ordpc) (void)hipFree(dev->d_ordpc);
     if (dev->d_segslots) (void)hipFree(dev->d_segslots);
     if (dev->d_work) (void)hipFree(dev->d_work);
@@ -1694,104 +1401,29 @@ static int ensure_buffer(T** p, size_t* cap, size_t bytes, char* err, size_t err
     return 0;
 }
 
-// The lane tracer's table: the program minus its binop records, BOUND skip
-// targets renumbered; plus ordinal -> program pc for the hit leaf.  Built only
-// for union-only programs (otherwise n_trav = 0 and the lane kernel is unused).
-static int build_trav(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n_prims, char* err, size_t errlen) {
-    dev->n_trav = 0;
-    dev->union_only = false;
+// Whether the program is union-only (the lane tracer's union count), and the
+// ordinal -> program pc map the lane tracer reads generic primitives and hit
+// leaves through.
+static int scene_maps(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n_prims, char* err, size_t errlen) {
     bool union_only = n_prims > 0;
-    for (uint32_t pc = 0; pc < n_recs && union_only;) {
-        uint32_t op = prog[pc].op;
+    std::vector<uint32_t> ordpc(n_prims ? n_prims : 1u, 0u);
+    for (uint32_t pc = 0; pc < n_recs;) {
+        const uint32_t op = prog[pc].op;
         if (op == WO_OP_PRIM) {
+            if (prog[pc].u1 < n_prims) ordpc[prog[pc].u1] = pc;
             pc += 1u + prog[pc].u0;
         } else {
             if (op != WO_OP_UNION && op != WO_OP_BOUND) union_only = false;
             ++pc;
         }
     }
-    if (!union_only) {
-        // the term mode of the lane tracer (build_lbvh) reads primitives through
-        // the ordinal -> program pc map too
-        std::vector<uint32_t> ordpc(n_prims ? n_prims : 1u, 0u);
-        for (uint32_t pc = 0; pc < n_recs;) {
-            if (prog[pc].op == WO_OP_PRIM) {
-                if (prog[pc].u1 < n_prims) ordpc[prog[pc].u1] = pc;
-                pc += 1u + prog[pc].u0;
-            } else {
-                ++pc;
-            }
-        }
-        if (ensure_buffer(&dev->d_ordpc, &dev->ordpc_cap, ordpc.size() * sizeof(uint32_t), err, errlen)) return -1;
-        hipError_t e = hipMemcpy(dev->d_ordpc, ordpc.data(), ordpc.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
-        if (e != hipSuccess) {
-            set_err(err, errlen, "hipMemcpy(ordinal map)", e);
-            return -1;
-        }
-        return 0;
-    }
-    // pass 1: node index of every program record (binops and leaves map to the next node)
-    std::vector<uint32_t> map(n_recs + 1u, 0u), ordpc(n_prims, 0u);
-    uint32_t nn = 0;
-    for (uint32_t pc = 0; pc < n_recs;) {
-        map[pc] = nn;
-        const WoRec& r = prog[pc];
-        if (r.op == WO_OP_PRIM) {
-            if (r.u1 < n_prims) ordpc[r.u1] = pc;
-            for (uint32_t m = 1; m <= r.u0; ++m) map[pc + m] = nn + 1u;
-            ++nn;
-            pc += 1u + r.u0;
-        } else {
-            if (r.op == WO_OP_BOUND) ++nn;
-            ++pc;
-        }
-    }
-    map[n_recs] = nn;
-    if (nn >= (1u << 30) || n_prims >= (1u << 30)) {
-        snprintf(err, errlen, "traversal table too large");
-        return -1;
-    }
-    // pass 2: geo (float4) then aux (u32), one buffer
-    std::vector<float4> geo(nn);
-    std::vector<uint32_t> aux(nn);
-    uint32_t k = 0;
-    for (uint32_t pc = 0; pc < n_recs;) {
-        const WoRec& r = prog[pc];
-        if (r.op == WO_OP_PRIM) {
-            const WoRec& L = prog[pc + 1u];
-            if (r.u0 == 1u && L.op == WO_LEAF_SPHERE) {
-                geo[k] = make_float4(L.f[0], L.f[1], L.f[2], L.f[3]);
-                aux[k] = (kNodeSphere << 30) | r.u1;
-            } else {
-                geo[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                aux[k] = (kNodeGeneric << 30) | r.u1;
-            }
-            ++k;
-            pc += 1u + r.u0;
-        } else {
-            if (r.op == WO_OP_BOUND) {
-                geo[k] = make_float4(r.f[0], r.f[1], r.f[2], r.f[4]);
-                aux[k] = (kNodeBound << 30) | (r.u0 <= n_recs ? map[r.u0] : nn);
-                ++k;
-            }
-            ++pc;
-        }
-    }
-    size_t bytes = (size_t)nn * (sizeof(float4) + sizeof(uint32_t));
-    if (ensure_buffer(&dev->d_trav, &dev->trav_cap, bytes, err, errlen)) return -1;
-    if (ensure_buffer(&dev->d_ordpc, &dev->ordpc_cap, (size_t)n_prims * sizeof(uint32_t), err, errlen)) return -1;
-    hipError_t e = hipMemcpy(dev->d_trav, geo.data(), (size_t)nn * sizeof(float4), hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = hipMemcpy((char*)dev->d_trav + (size_t)nn * sizeof(float4), aux.data(), (size_t)nn * sizeof(uint32_t),
-                      hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = hipMemcpy(dev->d_ordpc, ordpc.data(), (size_t)n_prims * sizeof(uint32_t), hipMemcpyHostToDevice);
+    dev->union_only = union_only;
+    if (ensure_buffer(&dev->d_ordpc, &dev->ordpc_cap, ordpc.size() * sizeof(uint32_t), err, errlen)) return -1;
+    hipError_t e = hipMemcpy(dev->d_ordpc, ordpc.data(), ordpc.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
-        set_err(err, errlen, "hipMemcpy(traversal table)", e);
+        set_err(err, errlen, "hipMemcpy(ordinal map)", e);
         return -1;
     }
-    dev->n_trav = nn;
-    dev->union_only = true;
     return 0;
 }
 
@@ -2125,117 +1757,7 @@ static bool extract_terms(WoRec const* prog, uint32_t n_recs, uint32_t n_prims,
     return true;
 }
 
-// Uniform grid over single-sphere primitives (the lane tracer's kMode 10,
-// WOLOLO_LANES_GRID=1): about `density` cells per primitive, cubic-ish cells over
-// the primitives' bounding box; each primitive is binned into every cell its box,
-// grown by kGridPad (more than t_min along a unit direction, and far more than the
-// DDA's rounding), overlaps, so the first cell holds every primitive containing the
-// ray's start and a cell the rounded walk visits instead of its true neighbour
-// still lists what the neighbour would.  Offsets (ncells + 1) then ordinals.
-static int build_grid(WoDev* dev, const std::vector<LbPrim>& prims, char* err, size_t errlen) {
-    constexpr double kGridPad = 4e-3;
-    if (prims.empty()) return 0;
-    double lo[3], hi[3];
-    for (int a = 0; a < 3; ++a) lo[a] = INFINITY, hi[a] = -INFINITY;
-    for (const LbPrim& p : prims)
-        for (int a = 0; a < 3; ++a) lo[a] = fmin(lo[a], p.lo[a] - kGridPad), hi[a] = fmax(hi[a], p.hi[a] + kGridPad);
-    double density = 3.0;
-    if (const char* v = getenv("WOLOLO_LANES_GRID_DENSITY")) density = v[0] ? strtod(v, NULL) : density;
-    double ext[3], vol = 1.0;
-    for (int a = 0; a < 3; ++a) ext[a] = fmax(hi[a] - lo[a], 1e-6), vol *= ext[a];
-    const double h = cbrt(vol / (density * (double)prims.size()));
-    uint32_t res[3];
-    for (int a = 0; a < 3; ++a) {
-        const double r = ceil(ext[a] / h);
-        res[a] = (uint32_t)(r < 1.0 ? 1.0 : (r > 512.0 ? 512.0 : r));
-    }
-    const uint64_t ncells = (uint64_t)res[0] * res[1] * res[2];
-    if (ncells > (1u << 24)) return 0;
-    float flo[3], fh[3];
-    for (int a = 0; a < 3; ++a) {
-        flo[a] = (float)lo[a];
-        fh[a] = (float)(ext[a] / res[a]);
-    }
-    auto cell_range = [&](const LbPrim& p, int a, uint32_t& c0, uint32_t& c1) {
-        const double x0 = (p.lo[a] - kGridPad - (double)flo[a]) / (double)fh[a];
-        const double x1 = (p.hi[a] + kGridPad - (double)flo[a]) / (double)fh[a];
-        const double m = (double)res[a] - 1.0;
-        c0 = (uint32_t)fmin(fmax(floor(x0), 0.0), m);
-        c1 = (uint32_t)fmin(fmax(floor(x1), 0.0), m);
-    };
-    std::vector<uint32_t> count(ncells + 1u, 0u);
-    for (int pass = 0; pass < 2; ++pass) {
-        std::vector<uint32_t> fill;
-        if (pass == 1) {
-            for (uint64_t c = 0; c < ncells; ++c) count[c + 1u] += count[c];  // exclusive offsets
-            fill.assign(count.begin(), count.end() - 1);
-        }
-        std::vector<uint32_t> items(pass == 1 ? count[ncells] : 0u);
-        for (const LbPrim& p : prims) {
-            uint32_t r0[3], r1[3];
-            for (int a = 0; a < 3; ++a) cell_range(p, a, r0[a], r1[a]);
-            for (uint32_t z = r0[2]; z <= r1[2]; ++z)
-                for (uint32_t y = r0[1]; y <= r1[1]; ++y)
-                    for (uint32_t x = r0[0]; x <= r1[0]; ++x) {
-                        const uint64_t c = ((uint64_t)z * res[1] + y) * res[0] + x;
-                        if (pass == 0)
-                            ++count[c + 1u];
-                        else
-                            items[fill[c]++] = p.ord;
-                    }
-        }
-        if (pass == 1) {
-            const size_t bytes = (count.size() + items.size()) * sizeof(uint32_t);
-            if (ensure_buffer(&dev->d_grid, &dev->grid_cap, bytes, err, errlen)) return -1;
-            std::vector<uint32_t> blob(count);
-            blob.insert(blob.end(), items.begin(), items.end());
-            hipError_t e = hipMemcpy(dev->d_grid, blob.data(), bytes, hipMemcpyHostToDevice);
-            if (e != hipSuccess) {
-                set_err(err, errlen, "hipMemcpy(lane grid)", e);
-                return -1;
-            }
-            dev->g_items_off = (uint32_t)count.size();
-        }
-    }
-    for (int a = 0; a < 3; ++a) {
-        dev->g_lo[a] = flo[a];
-        dev->g_h[a] = fh[a];
-        dev->g_res[a] = res[a];
-    }
-    dev->lb_grid = true;
-    return 0;
-}
-
-// Union-only programs: an AABB BVH over the bounded primitives (boxes expanded by
-// 1e-4 of their size and position plus 1e-5, so the approximate slab test never
-// culls a primitive the exact arithmetic meets) and the always list: unbounded
-// primitives and outsized ones (box diagonal > 16x the median, e.g. an RTIOW
-// ground sphere, which every ray meets anyway).  WOLOLO_LANES_BVH=0: none (the
-// general walk only).
-static uint32_t lb_node_f4(const WoDev* dev) { return dev->lb_wide ? 7u : (dev->lb_half ? 2u : 4u); }
-
-// fp16 bits of x rounded toward +inf (`up`) or -inf (host): the nearest fp16, one
-// step further when it lies on the wrong side of x (an overflow rounds to the
-// infinity on its side, which a box bound may be)
-static uint32_t half_dir(float x, bool up) {
-    const _Float16 h = (_Float16)x;
-    uint16_t b;
-    memcpy(&b, &h, sizeof b);
-    const float back = (float)h;
-    if (up && back < x) {
-        b = b == 0x8000u ? 0x0001u : (b & 0x8000u) ? (uint16_t)(b - 1u) : (b == 0x7c00u ? b : (uint16_t)(b + 1u));
-    } else if (!up && back > x) {
-        b = b == 0x0000u ? 0x8001u : (b & 0x8000u) ? (b == 0xfc00u ? b : (uint16_t)(b + 1u)) : (uint16_t)(b - 1u);
-    }
-    return b;
-}
-static uint32_t half_down(float x) { return half_dir(x, false); }
-static uint32_t half_up(float x) { return half_dir(x, true); }
-static uint32_t f_bits(float x) {
-    uint32_t u;
-    memcpy(&u, &x, sizeof u);
-    return u;
-}
+static uint32_t lb_node_f4(const WoDev* dev) { return dev->lb_wide ? 7u : 4u; }
 
 static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n_prims, WoMaterial const* mats,
                       uint32_t n_mats, char* err, size_t errlen) {
@@ -2245,17 +1767,11 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     dev->lb_spheres_only = false;
     dev->lb_stack16 = false;
     dev->lb_wide = false;
-    dev->lb_grid = false;
     dev->lb_terms = 0;
-    const char* env = getenv("WOLOLO_LANES_BVH");
-    if (env && env[0] == '0') return 0;
     // not union-only: the BVH over the root's terms, when the root is a union of
     // small conjunctions (extract_terms)
     std::vector<std::vector<uint32_t>> terms;
-    if (!dev->union_only) {
-        const char* tv = getenv("WOLOLO_LANES_TERMS");
-        if ((tv && tv[0] == '0') || !extract_terms(prog, n_recs, n_prims, terms)) return 0;
-    }
+    if (!dev->union_only && !extract_terms(prog, n_recs, n_prims, terms)) return 0;
     std::vector<LbPrim> prims;
     std::vector<uint32_t> always;
     std::vector<float4> geo(n_prims, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
@@ -2377,30 +1893,24 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
         }
         prims.swap(kept);
     }
-    {
-        // spheres only, union only: the uniform grid on request (WOLOLO_LANES_GRID=1)
-        const char* gv = getenv("WOLOLO_LANES_GRID");
-        const bool spheres = terms.empty() && std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
-        if (spheres && gv && gv[0] == '1' && build_grid(dev, prims, err, errlen)) return -1;
-    }
     std::vector<float4> nodes;
-    if (ceil_log2((uint32_t)prims.size()) > kLaneDepthMax) return 0;  // > 2^24 primitives: the general walk
+    if (ceil_log2((uint32_t)prims.size()) > kLaneDepthMax) {  // > 2^24 primitives (launches allow 2^20)
+        snprintf(err, errlen, "too many primitives for the lane BVH");
+        return -1;
+    }
     if (!prims.empty()) {
         // levels: SAH's freedom over the balanced tree's log2(n), within the stack's limit
+        // (the balanced tree, levels = log2(n): RTIOW cover 12.20 ms against 11.60)
         uint32_t levels = ceil_log2((uint32_t)prims.size()) + 6u;
-        const char* lv = getenv("WOLOLO_LANES_DEPTH");
-        if (lv && *lv) levels = (uint32_t)strtoul(lv, NULL, 10);
-        if (levels < ceil_log2((uint32_t)prims.size())) levels = ceil_log2((uint32_t)prims.size());
         if (levels > kLaneDepthMax) levels = kLaneDepthMax;
         LbBox root_box;
         dev->lb_root = lb_build(prims, 0u, (uint32_t)prims.size(), levels, nodes, root_box, dev->lb_depth);
-        // 4-wide nodes (WOLOLO_LANES_WIDE=1): refs must fit the 16-bit stack entries.
-        // Default for term mode over 256 terms (csg512_balanced, resumable walks: 50.1 ->
-        // 44.7 ms over the binary tree; non-resumable 82.0 -> 70.5); neutral on csg256
-        // balanced's 65 terms, 16.4 / 16.5 ms; slower on csg32's 14, 8.9 -> 9.6, and on
-        // the RTIOW cover's spheres, 11.7 -> 13.7
-        const char* wv = getenv("WOLOLO_LANES_WIDE");
-        const bool want_wide = wv && *wv ? wv[0] == '1' : (kLanesWideDefault || terms.size() > 256u);
+        // 4-wide nodes: refs must fit the 16-bit stack entries.  For term mode over 256
+        // terms (csg512_balanced, resumable walks: 50.1 -> 44.7 ms over the binary tree;
+        // non-resumable 82.0 -> 70.5); neutral on csg256 balanced's 65 terms, 16.4 / 16.5
+        // ms; slower on csg32's 14, 8.9 -> 9.6, and on the RTIOW cover's spheres, 11.7 ->
+        // 13.7
+        const bool want_wide = terms.size() > 256u;
         const uint32_t nrefs = terms.empty() ? n_prims : (uint32_t)terms.size();
         if (want_wide && !(dev->lb_root & kLeafRef) && nrefs < 0x8000u) {
             std::vector<float4> n4;
@@ -2445,43 +1955,19 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
             dev->lb_root = 0u;
         }
     }
-    // fp16 child boxes (WOLOLO_LANES_HALF=1; binary single-sphere trees, kind 15): each
-    // node's two children as 6 fp16 (lo rounded down, hi up) + ref = 2 x 16 bytes
-    {
-        const char* hv = getenv("WOLOLO_LANES_HALF");
-        const bool spheres = terms.empty() && std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
-        dev->lb_half = (hv && *hv ? hv[0] == '1' : kLanesHalfDefault) && spheres && !dev->lb_wide && !dev->lb_grid &&
-                       !nodes.empty() && !(dev->lb_root & kLeafRef);
-        if (dev->lb_half) {
-            const size_t nn = nodes.size() / 4u;
-            std::vector<float4> hn(2u * nn);
-            for (size_t i = 0; i < nn; ++i)
-                for (int c = 0; c < 2; ++c) {
-                    const float4 lo = nodes[4u * i + 2u * (uint32_t)c], hi = nodes[4u * i + 2u * (uint32_t)c + 1u];
-                    const uint32_t ref = f_bits(c == 0 ? nodes[4u * i].w : nodes[4u * i + 1u].w);
-                    const uint32_t q[3] = {half_down(lo.x) | half_down(lo.y) << 16, half_down(lo.z) | half_up(hi.x) << 16,
-                                           half_up(hi.y) | half_up(hi.z) << 16};
-                    hn[2u * i + (uint32_t)c] = make_float4(bits_f(q[0]), bits_f(q[1]), bits_f(q[2]), bits_f(ref));
-                }
-            nodes.swap(hn);
-        }
-    }
     const uint32_t node_f4 = lb_node_f4(dev);
     dev->lb_nodes = (uint32_t)(nodes.size() / node_f4);
     dev->lb_always = (uint32_t)always.size();
     {
-        // 16-bit stack entries when every ref fits 15 bits (WOLOLO_LANES_STACK16=1; always for 4-wide nodes)
-        const char* s16 = getenv("WOLOLO_LANES_STACK16");
-        dev->lb_stack16 = dev->lb_wide || (!dev->lb_half && terms.empty() && dev->lb_nodes < 0x8000u &&
-                                           n_prims < 0x8000u && s16 && s16[0] == '1');
+        // 16-bit stack entries for 4-wide nodes (binary trees: 32-bit, RTIOW cover
+        // 11.60 ms against 11.76 with 16-bit entries and more top nodes)
+        dev->lb_stack16 = dev->lb_wide;
         // the top nodes fill what the stacks leave of kLanesBvhLds (8 workgroups per CU)
         const size_t stacks =
             ((((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u)) + 15u) & ~(size_t)15u);
-        uint32_t top = stacks < kLanesBvhLds ? (uint32_t)((kLanesBvhLds - stacks) / (node_f4 * sizeof(float4))) : 0u;
-        const char* v = getenv("WOLOLO_LANES_TOP");
-        if (v && *v) top = (uint32_t)strtoul(v, NULL, 10);
+        const uint32_t top =
+            stacks < kLanesBvhLds ? (uint32_t)((kLanesBvhLds - stacks) / (node_f4 * sizeof(float4))) : 0u;
         dev->lb_top = top < dev->lb_nodes ? top : dev->lb_nodes;
-        if (dev->lb_grid) dev->lb_top = 0;  // the grid walk reads no nodes
     }
     dev->lb_spheres_only = terms.empty() && std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
     dev->lb_terms = (uint32_t)terms.size();
@@ -2532,17 +2018,7 @@ static LaneBvh lane_bvh(const WoDev* dev) {
     b.nprims = dev->lb_nprims;
     b.ntop = dev->lb_top;
     b.depth = dev->lb_depth;
-    b.dyn_walkers = 24u;  // measured: tools/env_ab.sh rtiow_cover
-    if (const char* v = getenv("WOLOLO_LANES_DYN_WALKERS"))
-        if (*v) b.dyn_walkers = (uint32_t)strtoul(v, NULL, 10);
-    for (int a = 0; a < 3; ++a) {
-        b.glo[a] = dev->g_lo[a];
-        b.gh[a] = dev->g_h[a];
-        b.ginv[a] = dev->lb_grid ? 1.0f / dev->g_h[a] : 0.0f;
-        b.gres[a] = dev->g_res[a];
-    }
-    b.gcells = dev->lb_grid ? dev->d_grid : nullptr;
-    b.gitems = dev->lb_grid ? dev->d_grid + dev->g_items_off : nullptr;
+    b.dyn_walkers = 24u;  // csg512_balanced: 60.4 / 57.6 / 57.2 / 58.1 / 59.2 ms at 8 / 16 / 24 / 32 / 40
     b.trec = dev->lb_terms ? reinterpret_cast<const float4*>(reinterpret_cast<const uint32_t*>(dev->d_lbvh) +
                                                             dev->lb_term_off)
                            : nullptr;
@@ -2587,7 +2063,7 @@ extern "C" int wo_dev_upload_scene(WoDev* dev, WoRec const* prog, uint32_t n_rec
     dev->n_recs = n_recs;
     dev->n_prims = n_prims;
     dev->n_mats = n_mats;
-    if (build_trav(dev, prog, n_recs, n_prims, err, errlen)) return -1;
+    if (scene_maps(dev, prog, n_recs, n_prims, err, errlen)) return -1;
     return build_lbvh(dev, prog, n_recs, n_prims, mats, n_mats, err, errlen);
 }
 
@@ -2912,8 +2388,7 @@ extern "C" double wo_dev_jit_compile_sec(WoDev* dev) { return dev ? dev->jit_com
 // 4 / 8 (8x8 tiles throughout); 3-round tail 5.50 / 2.81 / 1.53 / 0.81 ms.  The big shape is 8x8
 // while the frame holds >= 8 rounds of such tiles, else 8x4 (2-round tail), else 4x4
 // (plan_tiles); `resident` = workgroups the device holds at once.  Env (measurements):
-// WOLOLO_TILE=8x8|8x4|4x4 forces one shape everywhere (plus a tail only when
-// WOLOLO_TILE_TAIL is set); WOLOLO_TILE_TAIL=<rounds> sets the tail (0: none).
+// WOLOLO_TILE=8x8|8x4|4x4 forces one shape everywhere, with no tail.
 // "WxH" with W, H in {1, 2, 4, 8} and W*H <= kTileMaxPix; 0 if not such a shape
 static uint32_t shape_of(const char* f) {
     unsigned w = 0, h = 0;
@@ -2928,21 +2403,17 @@ static uint32_t tiles_across(uint32_t width, uint32_t shape) { return (width + (
 static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, uint32_t band_rows) {
     const uint32_t s44 = 2u | (2u << 4);
     PathLaunch g = {};
-    uint32_t small = s44;
-    {
-        const char* sv = getenv("WOLOLO_TILE_SMALL");
-        if (sv && *sv && shape_of(sv)) small = shape_of(sv);
-    }
+    // the tail's tiles: 4x4 (2x2 / 4x2 for an 8-rank share's tail: within noise,
+    // DESIGN.md §6)
+    const uint32_t small = s44;
     g.small_log2 = small;
     g.tiles_x_small = tiles_across(width, small);
     const uint32_t sh = 1u << (small >> 4);
-    double tail_rounds = 3.0;
-    const char* tv = getenv("WOLOLO_TILE_TAIL");
-    if (tv && *tv) tail_rounds = atof(tv);
-    const char* f = getenv("WOLOLO_TILE");
+    double tail_rounds = 3.0;  // rounds of resident workgroups in the tail
+    const char* f = getenv("WOLOLO_TILE");  // a forced tile shape ("8x4"): the whole frame in it
     uint32_t big = (f && *f) ? shape_of(f) : 0u;
     if (big) {
-        if (!(tv && *tv)) tail_rounds = 0.0;  // a forced shape covers the frame unless a tail is asked for
+        tail_rounds = 0.0;
     } else {
         // The largest shape that gives every resident workgroup >= 8 tiles: a
         // workgroup's tiles then average out the costly ones (glass, deep CSG),
@@ -2956,7 +2427,7 @@ static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, u
         big = 3u | (3u << 4);
         if ((uint64_t)tiles_across(width, big) * (rows >> 3) < want_tiles || band_rows < 8u) {
             big = 3u | (2u << 4);
-            if (!(tv && *tv)) tail_rounds = 2.0;
+            tail_rounds = 2.0;
         }
         if ((uint64_t)tiles_across(width, big) * (rows >> 2) < want_tiles) big = s44;
     }
@@ -2977,53 +2448,27 @@ static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, u
 
 static const size_t kLdsBudget = 64u * 1024u;
 // Lane-traversal nodes in LDS: up to ~1200 nodes keeps 6 workgroups per CU
-// (24 KB + 7 KB of sample accumulators each).
-static const size_t kLanesLdsBudget = 24u * 1024u;
 
 extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, void* stream_v,
                              unsigned long long* d_segments, char* err, size_t errlen) {
     return wo_dev_launch_ex(dev, frame_in, d_out, stream_v, d_segments, nullptr, 0u, err, errlen);
 }
 
-enum PathKind { kLanesLds, kLanesGlobal, kLanesBvh, kLanesBvhSpheres, kLanesBvh16, kLanesBvhSpheres16, kLanesTerms,
-                kLanesWideSpheres, kLanesWide, kLanesWideTerms, kLanesGrid, kLanesDynSpheres, kLanesDyn, kLanesDynTerms,
-                kLanesDynWideTerms, kLanesBvhSpheresHalf, kJit, kInterpLds, kInterpGlobal };
+// the numbers are wo_renderer_lanes_info's "kind" (the lane tracer's forms, LaneTracer)
+enum PathKind { kLanesBvh = 2, kLanesBvhSpheres = 3, kLanesTerms = 6, kLanesDynWideTerms = 14, kJit = 16, kInterpLds = 17,
+                kInterpGlobal = 18 };
 
 template <bool kCount>
 static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
     switch (kind) {
-    case kLanesLds:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<0, kCount>, kBlock, dyn_lds);
-    case kLanesGlobal:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<1, kCount>, kBlock, dyn_lds);
     case kLanesBvh:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<2, kCount>, kBlock, dyn_lds);
     case kLanesBvhSpheres:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<3, kCount>, kBlock, dyn_lds);
-    case kLanesBvh16:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<4, kCount>, kBlock, dyn_lds);
-    case kLanesBvhSpheres16:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<5, kCount>, kBlock, dyn_lds);
     case kLanesTerms:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<6, kCount>, kBlock, dyn_lds);
-    case kLanesWideSpheres:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<7, kCount>, kBlock, dyn_lds);
-    case kLanesWide:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<8, kCount>, kBlock, dyn_lds);
-    case kLanesWideTerms:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<9, kCount>, kBlock, dyn_lds);
-    case kLanesGrid:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<10, kCount>, kBlock, dyn_lds);
-    case kLanesDynSpheres:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<11, kCount>, kBlock, dyn_lds);
-    case kLanesDyn:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<12, kCount>, kBlock, dyn_lds);
-    case kLanesDynTerms:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<13, kCount>, kBlock, dyn_lds);
     case kLanesDynWideTerms:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<14, kCount>, kBlock, dyn_lds);
-    case kLanesBvhSpheresHalf:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<15, kCount>, kBlock, dyn_lds);
     case kInterpLds:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_kernel<true, kCount>, kBlock, dyn_lds);
     default:
@@ -3031,90 +2476,29 @@ static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
     }
 }
 
+template <int kMode, bool kCount>
+static void lanes_launch(dim3 grid, size_t dyn_lds, hipStream_t stream, WoDev* dev, const WoFrame& fr,
+                         uint32_t local_rows, float4* out, unsigned long long* slots, const PathLaunch& tg) {
+    hipLaunchKernelGGL((pathtrace_lanes_kernel<kMode, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
+                       dev->d_ordpc, dev->d_mats, fr, local_rows, out, slots, tg, lane_bvh(dev));
+}
+
 template <bool kCount>
 static void static_launch(PathKind kind, dim3 grid, size_t dyn_lds, hipStream_t stream, WoDev* dev, const WoFrame& fr,
                           const KLayout& lay, uint32_t local_rows, float4* out, unsigned long long* slots,
                           const PathLaunch& tg) {
     switch (kind) {
-    case kLanesLds:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<0, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
-        break;
-    case kLanesGlobal:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<1, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
-        break;
     case kLanesBvh:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<2, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
+        lanes_launch<2, kCount>(grid, dyn_lds, stream, dev, fr, local_rows, out, slots, tg);
         break;
     case kLanesBvhSpheres:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<3, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
-        break;
-    case kLanesBvh16:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<4, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
-        break;
-    case kLanesBvhSpheres16:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<5, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
+        lanes_launch<3, kCount>(grid, dyn_lds, stream, dev, fr, local_rows, out, slots, tg);
         break;
     case kLanesTerms:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<6, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
-        break;
-    case kLanesWideSpheres:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<7, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
-        break;
-    case kLanesWide:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<8, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
-        break;
-    case kLanesWideTerms:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<9, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
-        break;
-    case kLanesGrid:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<10, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
-        break;
-    case kLanesDynSpheres:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<11, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
-        break;
-    case kLanesDyn:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<12, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
-        break;
-    case kLanesDynTerms:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<13, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
+        lanes_launch<6, kCount>(grid, dyn_lds, stream, dev, fr, local_rows, out, slots, tg);
         break;
     case kLanesDynWideTerms:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<14, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
-        break;
-    case kLanesBvhSpheresHalf:
-        hipLaunchKernelGGL((pathtrace_lanes_kernel<15, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
-                           dev->d_trav, dev->d_ordpc, dev->d_mats, fr, dev->n_trav, local_rows, out, slots, tg,
-                           lane_bvh(dev));
+        lanes_launch<14, kCount>(grid, dyn_lds, stream, dev, fr, local_rows, out, slots, tg);
         break;
     case kInterpLds:
         hipLaunchKernelGGL((pathtrace_kernel<true, kCount>), grid, dim3(kBlock), dyn_lds, stream, dev->d_prog,
@@ -3190,36 +2574,16 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
         size_t dyn_lds = 0;
         KLayout lay = {};
         if (dev->lanes_on && (dev->union_only || dev->lb_terms) && !dev->jit_fn) {
-            // the ordered BVH: the lane stacks in LDS; the general walk: its table
-            // in LDS when it fits
-            const size_t table = (size_t)dev->n_trav * (sizeof(float4) + sizeof(uint32_t));
-            if (dev->lb_root != kNoRef || dev->lb_always != 0u) {
-                if (dev->lb_grid)
-                    kind = kLanesGrid;
-                else if (dev->lb_wide)
-                    kind = dev->lb_terms ? kLanesWideTerms : (dev->lb_spheres_only ? kLanesWideSpheres : kLanesWide);
-                else
-                    kind = dev->lb_terms   ? kLanesTerms
-                           : dev->lb_stack16 ? (dev->lb_spheres_only ? kLanesBvhSpheres16 : kLanesBvh16)
-                                             : (dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh);
-                // the resumable walk (dynamic ray fetch) for the binary 32-bit-stack forms
-                // and 4-wide term mode: WOLOLO_LANES_DYN=1 (or 0) over the default, which is
-                // term mode over more than 256 terms (csg512_balanced 84.3 -> 56.4 ms; slower
-                // where walks are short or alike: the RTIOW cover 11.7 -> 12.9-15.5 ms,
-                // csg256 balanced's 65 terms 16.5 -> 18.2)
-                const char* dv = getenv("WOLOLO_LANES_DYN");
-                const bool dyn = dv && *dv ? dv[0] == '1' : (kLanesDynDefault || dev->lb_terms > 256u);
-                if (dyn && kind == kLanesBvhSpheres) kind = kLanesDynSpheres;
-                else if (dyn && kind == kLanesBvh) kind = kLanesDyn;
-                else if (dyn && kind == kLanesTerms) kind = kLanesDynTerms;
-                else if (dyn && kind == kLanesWideTerms) kind = kLanesDynWideTerms;
-                if (dev->lb_half && kind == kLanesBvhSpheres) kind = kLanesBvhSpheresHalf;
-                const size_t stacks = ((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u) + 15u) & ~(size_t)15u;
-                dyn_lds = dev->lb_grid ? 0u : stacks + (size_t)dev->lb_top * lb_node_f4(dev) * sizeof(float4);
-            } else {
-                kind = table <= kLanesLdsBudget ? kLanesLds : kLanesGlobal;
-                dyn_lds = kind == kLanesLds ? table : 0u;
-            }
+            // the ordered BVH, its lane stacks and top nodes in LDS.  Term mode over more
+            // than 256 terms: the 4-wide tree with the resumable walk (dynamic ray fetch;
+            // csg512_balanced 84.3 -> 44.7 ms; slower where walks are short or alike: the
+            // RTIOW cover 11.7 -> 12.9-15.5 ms, csg256 balanced's 65 terms 16.5 -> 18.2;
+            // DESIGN.md §3.6c)
+            kind = dev->lb_wide ? kLanesDynWideTerms
+                   : dev->lb_terms ? kLanesTerms
+                   : (dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh);
+            const size_t stacks = ((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u) + 15u) & ~(size_t)15u;
+            dyn_lds = stacks + (size_t)dev->lb_top * lb_node_f4(dev) * sizeof(float4);
         } else if (dev->jit_fn) {
             kind = kJit;
         } else {

@@ -209,8 +209,8 @@ int wo_renderer_frame_desc(Wo_Renderer* r, Wo_RenderParams const* params, uint32
  *                (else, or if compilation fails, the interpreter).
  *   LANES        per-lane BOUND traversal, for union-only scenes (others fall
  *                back to AUTO's choice).
- * Environment: WOLOLO_TRACER=auto|interpreter|jit|lanes sets the initial value;
- * WOLOLO_JIT=0 means interpreter.  Takes effect at the next render. */
+ * Environment: WOLOLO_TRACER=auto|interpreter|jit|lanes sets the initial value.
+ * Takes effect at the next render. */
 typedef enum Wo_Tracer {
     WO_TRACER_AUTO = 0,
     WO_TRACER_INTERPRETER = 1,

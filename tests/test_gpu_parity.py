@@ -423,14 +423,10 @@ def _union_scene(n_spheres=90):
     return r
 
 
-@pytest.mark.parametrize("stack16", [None, "1"])
 @pytest.mark.parametrize("tracer", ["lanes", "auto"])
-def test_lanes_union_scene_bitexact(tracer, stack16, monkeypatch):
-    # AUTO takes the lane tracer for union-only scenes above WOLOLO_LANES_MIN_PRIMS (256 by default);
-    # the BVH walk's stack has 32-bit entries by default, 16-bit ones with WOLOLO_LANES_STACK16=1
+def test_lanes_union_scene_bitexact(tracer, monkeypatch):
+    # AUTO takes the lane tracer for union-only scenes above WOLOLO_LANES_MIN_PRIMS (256 by default)
     monkeypatch.setenv("WOLOLO_LANES_MIN_PRIMS", "64")
-    if stack16 is not None:
-        monkeypatch.setenv("WOLOLO_LANES_STACK16", stack16)
     r = _union_scene()
     assert _union_only(r) and r.program()[2] > 64
     r.set_tracer(tracer)
@@ -443,15 +439,11 @@ def test_lanes_union_scene_bitexact(tracer, stack16, monkeypatch):
     r.close()
 
 
-@pytest.mark.parametrize("levels", [None, "0"])
-def test_lanes_bvh_depth_bound(levels, monkeypatch):
+def test_lanes_bvh_depth_bound(monkeypatch):
     """A chain of spheres at exponentially growing spacing: binned SAH splits off one
     far sphere at a time, a tree as deep as the scene is long without the depth
-    bound.  build_lbvh bounds the depth (log2(n) + 6 levels by default; a request below
-    log2(n), here 0, gives the balanced tree) so the per-lane LDS stack, sized by the
-    depth, never overflows, and the image stays the oracle's."""
-    if levels is not None:
-        monkeypatch.setenv("WOLOLO_LANES_DEPTH", levels)
+    bound.  build_lbvh bounds the depth (log2(n) + 6 levels) so the per-lane LDS
+    stack, sized by the depth, never overflows, and the image stays the oracle's."""
     monkeypatch.setenv("WOLOLO_LANES_MIN_PRIMS", "64")
     r = wl.Renderer("deep", max_nodes=4096)
     n = 600
@@ -472,37 +464,29 @@ def test_lanes_bvh_depth_bound(levels, monkeypatch):
     assert r.trace_path() == "lanes"
     info = r.lanes_info()
     log2n = int(np.ceil(np.log2(n)))
-    assert info["depth"] <= (log2n if levels == "0" else log2n + 6), info
+    assert info["depth"] <= log2n + 6, info
     assert info["nodes"] == n - info["always"] - 1  # a binary tree over the boxed primitives
     ref, _ = _oracle_rows(r, p)
-    _cmp(img, ref, f"deep chain, levels={levels}")
+    _cmp(img, ref, "deep chain")
     r.close()
 
 
-@pytest.mark.parametrize("knob,scene", [("WOLOLO_LANES_WIDE", s) for s in
-                                        ["union90", "rtiow_cover", "csg32", "csg256_balanced", "deep600"]] +
-                         [("WOLOLO_LANES_GRID", s) for s in ["rtiow_cover", "deep600", "glass200"]] +
-                         [("WOLOLO_LANES_DYN", s) for s in
-                          ["union90", "rtiow_cover", "csg32", "csg256_balanced", "deep600", "glass200"]] +
-                         [("WOLOLO_LANES_HALF", s) for s in ["rtiow_cover", "deep600", "glass200", "rtiow16"]])
-def test_lanes_wide_bvh_bitexact(knob, scene, monkeypatch):
-    """4-wide lane BVH (WOLOLO_LANES_WIDE=1, lb_collapse4): spheres-only (rtiow), generic
-    primitives (boxes, half-spaces: the union scene) and term mode (csg32, csg256 balanced),
-    and the 600-sphere chain whose tree is as deep as the depth bound allows (its 16-bit
-    stack holds 3 entries per level); every image the oracle's bit for bit.  The same
-    scenes of single spheres through the uniform grid (WOLOLO_LANES_GRID=1, build_grid:
-    a DDA walk), and a cluster of overlapping glass spheres (rays that start inside).
-    The resumable walk (WOLOLO_LANES_DYN=1: a wave's walking lanes bail out once few
-    lanes walk, the others shade and fetch new rays) on the binary forms (generic
-    primitives, single spheres, term mode, the deep chain and the glass cluster) and on
-    4-wide term mode.  Binary single-sphere trees with fp16 child boxes (WOLOLO_LANES_HALF=1:
-    lo rounded down and hi up, so a box only grows and the culling stays conservative)."""
-    monkeypatch.setenv(knob, "1")
-    if scene == "rtiow16":  # fp16 nodes asked for together with 16-bit stacks: the fp16 form (its 32-bit stack)
-        monkeypatch.setenv("WOLOLO_LANES_STACK16", "1")
-        scene = "rtiow_cover"
-    if knob == "WOLOLO_LANES_DYN" and scene == "csg256_balanced":
-        monkeypatch.setenv("WOLOLO_LANES_WIDE", "1")  # term mode's resumable 4-wide walk (kind 14)
+# the lane tracer's form per scene (PathKind: 2 generic primitives, 3 single spheres,
+# 6 term mode over <= 256 terms, 14 the resumable 4-wide term-mode walk)
+_LANE_KIND = {"union90": 2, "rtiow_cover": 3, "deep600": 3, "glass200": 3, "csg32": 6, "csg256_balanced": 6,
+              "csg512_balanced": 14}
+
+
+@pytest.mark.parametrize("scene", ["union90", "rtiow_cover", "csg32", "csg256_balanced", "deep600", "glass200",
+                                   "csg512_balanced"])
+def test_lane_tracer_forms_bitexact(scene, monkeypatch):
+    """Every form of the lane tracer, each on the scenes that take it: the binary walk
+    over generic primitives (boxes, half-spaces: the union scene), over single spheres
+    (the RTIOW cover; the 600-sphere chain whose tree is as deep as the depth bound
+    allows; a cluster of overlapping glass spheres, rays that start inside), term mode
+    over <= 256 terms (csg32, csg256 balanced) and the resumable 4-wide term-mode walk
+    (csg512_balanced: a wave's walking lanes bail out once few lanes walk, the others
+    shade and fetch new rays); every image the oracle's bit for bit."""
     monkeypatch.setenv("WOLOLO_LANES_MIN_PRIMS", "64")
     if scene == "union90":
         r = _union_scene()
@@ -545,15 +529,11 @@ def test_lanes_wide_bvh_bitexact(knob, scene, monkeypatch):
         img = r.render(p)
         assert r.trace_path() == "lanes"
         ref, _ = _oracle_rows(r, p)
-        _cmp(img, ref, f"wide {scene} mode={mode}")
+        _cmp(img, ref, f"lanes {scene} mode={mode}")
     info = r.lanes_info()
-    if knob == "WOLOLO_LANES_WIDE":
+    assert info["kind"] == _LANE_KIND[scene], info
+    if info["kind"] == 14:
         assert info["depth"] % 3 == 0 and info["depth"] <= 3 * 24, info  # 3 stack entries per 4-wide level
-    if knob == "WOLOLO_LANES_HALF":
-        assert info["kind"] == 15, info  # PathKind kLanesBvhSpheresHalf: fp16 child boxes
-    if knob == "WOLOLO_LANES_DYN":
-        # PathKind kLanesDynSpheres / kLanesDyn / kLanesDynTerms / kLanesDynWideTerms
-        assert info["kind"] == {"csg32": 13, "csg256_balanced": 14, "union90": 12}.get(scene, 11), info
     r.close()
 
 
@@ -574,12 +554,12 @@ def test_auto_tracer_choices():
         r.close()
 
 
-@pytest.mark.parametrize("window", ["lds2", "lds", "registers"])
+@pytest.mark.parametrize("window", ["lds2", "default"])
 def test_jit_event_windows(window, monkeypatch):
-    """The specialised kernel's two event windows (LDS list, register window) and
-    the LDS list's overflow barrier (capacity 2 forces it on most rays that meet
-    more than one primitive) all give the oracle's frame."""
-    monkeypatch.setenv("WOLOLO_JIT_LDS_EVENTS", "0" if window == "registers" else "1")
+    """The specialised kernel's event windows -- the sorted LDS list (csg32_nested),
+    the register window (csg256_chain) -- and the LDS list's overflow barrier
+    (capacity 2 forces it on most rays that meet more than one primitive) all give
+    the oracle's frame."""
     if window == "lds2":
         monkeypatch.setenv("WOLOLO_JIT_FLAGS", "-DWO_LDS_EVENTS=2")
     for name in ["csg32", "csg32_nested", "csg256_chain"]:
@@ -592,40 +572,27 @@ def test_jit_event_windows(window, monkeypatch):
         r.close()
 
 
-@pytest.mark.parametrize("knobs", [
-    {"WOLOLO_JIT_MEMBER_SKIP": "0", "WOLOLO_JIT_BOUND_SINGLE": "1"},
-    {"WOLOLO_JIT_MEMBER_SKIP": "1", "WOLOLO_JIT_BOUND_SINGLE": "1"},
-    {"WOLOLO_MEMBER_ORDER": "0"},
-    {"WOLOLO_JIT_FLAGS": "-DWO_LDS_NEXT_EAGER=0"},
-    {"WOLOLO_JIT_FLAGS": "-DWO_LDS_NEXT_EAGER=7"},
-    {"WOLOLO_JIT_FLAGS": "-DWO_LDS_EVENTS=2 -DWO_LDS_NEXT_EAGER=7"},  # eager reads clamped to the list
-    {"WOLOLO_JIT_SPATIAL": "1"},  # spatial groups instead of the union clusters' bounds
-    {"WOLOLO_JIT_SPATIAL": "1", "WOLOLO_JIT_SPATIAL_LEAF": "1"},
-    {"WOLOLO_JIT_SPATIAL": "0", "WOLOLO_JIT_UNION_COUNT": "0", "WOLOLO_JIT_DL_EVAL": "0"},
-    {"WOLOLO_JIT_FLAGS": "-DWO_LDS_KEEP_SMALLEST=0"},  # a full event list keeps its first keys
-    {"WOLOLO_JIT_FLAGS": "-DWO_LDS_EVENTS=3"},  # ... or its 3 smallest (overflow on most nested rays)
-    {"WOLOLO_JIT_TERMS": "1"},  # term transitions on csg256 balanced too (by default <= 64 primitives)
-    {"WOLOLO_JIT_TERMS": "0"},  # the event-list form on csg32
-    {"WOLOLO_JIT_TERMS": "1", "WOLOLO_JIT_DIST_CULL": "1"},  # groups beyond every lane's best skipped
-    {"WOLOLO_JIT_TERMS": "1", "WOLOLO_JIT_TERM_DIST": "1", "WOLOLO_JIT_KEY_VMOV": "1"},  # terms beyond a lane's best
-    {"WOLOLO_JIT_CULL_BARRIER": "1"},  # cull words through the opaque move in sweep steps too (nested: LDS list)
-    {"WOLOLO_JIT_CULL_BARRIER": "0"},  # no opaque move (the hoisted masks)
+@pytest.mark.parametrize("flags", [
+    "-DWO_LDS_NEXT_EAGER=0",
+    "-DWO_LDS_NEXT_EAGER=7",
+    "-DWO_LDS_EVENTS=2 -DWO_LDS_NEXT_EAGER=7",  # eager reads clamped to the list
+    "-DWO_LDS_KEEP_SMALLEST=0",  # a full event list keeps its first keys
+    "-DWO_LDS_EVENTS=3",  # ... or its 3 smallest (overflow on most nested rays)
+    "-DWO_SORTED_EVENTS=0",  # csg32_nested's list scanned per event instead of sorted once
 ])
-def test_jit_culling_knobs(knobs, monkeypatch):
-    """The wave-level member skip, the bound-around-a-lone-primitive rule, the
-    scene compiler's sphere-member order and the sweep's eager event reads change
-    how much work a wave does, never the image: every setting gives the oracle's
-    frame on the scenes with multi-member primitives (csg32's lenses and rounded
-    cube, csg256 balanced's 21 sphere intersections)."""
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
+def test_jit_compile_flag_variants(flags, monkeypatch):
+    """The event list's compile-time variants (WOLOLO_JIT_FLAGS) change how much work a
+    wave does, never the image: every setting gives the oracle's frame on the scenes
+    with multi-member primitives (csg32's lenses and rounded cube, csg32_nested's
+    boxes, csg256 balanced's 21 sphere intersections)."""
+    monkeypatch.setenv("WOLOLO_JIT_FLAGS", flags)
     for name in ["csg32", "csg32_nested", "csg256_balanced"]:
         r, info = _scene(name, "jit")
         p = info.params(width=64, height=36, spp=4, seed=13)
         img = r.render(p)
         _check_path(r, "jit")
         ref, _ = _oracle_rows(r, p)
-        _cmp(img, ref, f"{name} {knobs}")
+        _cmp(img, ref, f"{name} {flags}")
         r.close()
 
 

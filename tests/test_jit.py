@@ -10,39 +10,40 @@ from csgrenderer_amd import scenes
 from csgrenderer_amd import wololo as wl
 
 
-def test_csg32_source_compiles_for_gfx950(hostonly, monkeypatch):
-    # the event-list form (WOLOLO_JIT_TERMS=0) with the scene compiler's BOUND records as
-    # the culling structure (WOLOLO_JIT_SPATIAL=0); the spatial groups and the default
-    # term form are checked at the end
-    monkeypatch.setenv("WOLOLO_JIT_TERMS", "0")
-    monkeypatch.setenv("WOLOLO_JIT_SPATIAL", "0")
+_SINGLE_RE = r"wodev::(sphere_interval|sphere_interval_bd|sphere_need|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\("
+
+
+def _leaf_calls(src):
+    """(single-leaf interval calls, slab face-pair calls) in the generated source: a
+    sphere with literal constants ends in sphere_interval_bd, or is a lone sphere
+    tested with sphere_need; an axis face ends in halfspace_axis_dist; two opposite
+    faces of a slab are one axis_pair_meet."""
+    return len(re.findall(_SINGLE_RE, src)), len(re.findall(r"wodev::axis_pair_meet(_d)?\(", src))
+
+
+def test_generated_sources_compile_for_gfx950(hostonly):
+    """The three forms the generator picks by scene, each compiled by hiprtc for gfx950:
+    the event list with the scene compiler's BOUND records as the culling structure
+    (csg256_balanced: > 64 primitives in a shallow tree), the event list with spatial
+    groups (csg32_nested: a general root over <= 64 primitives, two boxes), and term
+    mode (csg32: a union of <= 2-literal conjunctions)."""
+    # BOUND records: wave-level tests only for subtrees of >= 4 leaves and not around a
+    # lone primitive (its member skip is the cheaper test)
     r = wl.Renderer("jit", max_nodes=4096)
-    scenes.build("csg32", r)
+    scenes.build("csg256_balanced", r)
     prog, nrec, nprim = r.program()
     src = r.jit_source()
-    assert src is not None
-    # one intersection call per leaf (a slab's two opposite faces: one pair call) in
-    # each of the two collect passes (first pass, re-collect), one cull flag per
-    # BOUND, ordinal table of every primitive
     nleaf = sum(1 for i in range(nrec) if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE))
-    # (a sphere with literal constants ends in sphere_interval_bd, or is a lone sphere tested with
-    # sphere_need; an axis face ends in halfspace_axis_dist)
-    nsingle = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|sphere_need|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
-    npair = len(re.findall(r"wodev::axis_pair_meet(_d)?\(", src))
-    assert npair >= 2 * 6  # the slab and the cube: three face pairs each, in both passes
-    assert nsingle + 2 * npair == 2 * nleaf
-    # the slab and the cube are axis-aligned: tagged by the compiler, emitted on the fast path
-    naxis = sum(1 for i in range(nrec) if prog[i].op == wl.WO_LEAF_HALFSPACE and prog[i].u1 != 0)
-    assert naxis >= 12
-    assert len(re.findall(r"wodev::halfspace_axis_(interval|dist)\(", src)) + 2 * npair == 2 * naxis
-    # wave-level tests only for BOUND subtrees of >= 4 leaves (scene_jit.c, WOLOLO_JIT_BOUND_MIN_LEAVES)
-    # and not around a lone primitive (WOLOLO_JIT_BOUND_SINGLE=0: its member skip is the cheaper test)
+    nsingle, npair = _leaf_calls(src)
+    assert nsingle + 2 * npair == 2 * nleaf  # every leaf in both collect passes
+
     def lone(i):
         return prog[i + 1].op == wl.WO_OP_PRIM and i + 2 + prog[i + 1].u0 == prog[i].u0
 
     nb = sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND and prog[i].u1 >= 4 and not lone(i))
     assert 0 < nb < sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_BOUND)
-    assert len(re.findall(r"if \(__ballot\((wodev::bound_may_hit\(|!miss\) == 0ull)", src)) == nb
+    assert len(re.findall(r"if \(__ballot\(!miss\) == 0ull\)", src)) == nb
+    assert "// group" not in src and "kUTerm" in src  # the union count of its pair terms
     m = re.search(r"kOrdPc\[(\d+)\] = \{([^}]*)\}", src)
     assert int(m.group(1)) == nprim
     pcs = [int(x.strip().rstrip("u")) for x in m.group(2).split(",")]
@@ -50,34 +51,40 @@ def test_csg32_source_compiles_for_gfx950(hostonly, monkeypatch):
     log = wl.jit_compile_check(src, "gfx950")
     assert log == "", log
     r.close()
-    # default for a small scene: the primitives grouped spatially (scene_jit.c gen_spatial),
-    # one wave-level test per group, no BOUND record tested; every leaf still intersected in both passes
-    monkeypatch.delenv("WOLOLO_JIT_SPATIAL")
+    # spatial groups: one wave-level test per group, no BOUND record tested; every leaf
+    # still intersected in both passes; the two boxes' axis faces on the fast path
     r = wl.Renderer("jit", max_nodes=4096)
-    scenes.build("csg32", r)
+    scenes.build("csg32_nested", r)
+    prog, nrec, nprim = r.program()
     src = r.jit_source()
+    nleaf = sum(1 for i in range(nrec) if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE))
     ngroups = len(re.findall(r"// group \d+ \((\d+) primitives\)", src))  # the first pass tests them
     assert ngroups >= 2 and "// BOUND" not in src
     assert len(re.findall(r"if \(__ballot\(!miss\) == 0ull\)", src)) == ngroups
-    nsingle = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|sphere_need|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
-    npair = len(re.findall(r"wodev::axis_pair_meet(_d)?\(", src))
+    nsingle, npair = _leaf_calls(src)
+    assert npair >= 2 * 6  # two boxes: three face pairs each, in both passes
     assert nsingle + 2 * npair == 2 * nleaf
+    naxis = sum(1 for i in range(nrec) if prog[i].op == wl.WO_LEAF_HALFSPACE and prog[i].u1 != 0)
+    assert naxis >= 12
+    assert len(re.findall(r"wodev::halfspace_axis_(interval|dist)\(", src)) + 2 * npair == 2 * naxis
+    assert "#define WO_SORTED_EVENTS 1" in src and "WO_EVAL_BEGIN" in src  # the sorted event list, a general root
     assert wl.jit_compile_check(src, "gfx950") == ""
     r.close()
-    # default: the term form (the root is a union of <= 2-literal conjunctions): every leaf
-    # still intersected once per pass, each term once per pass, no event list, no sweep
-    monkeypatch.delenv("WOLOLO_JIT_TERMS")
+    # the term form (the root is a union of <= 2-literal conjunctions): every leaf still
+    # intersected once per pass, each term once per pass, no event list, no sweep
     r = wl.Renderer("jit", max_nodes=4096)
     scenes.build("csg32", r)
+    prog, nrec, nprim = r.program()
     src = r.jit_source()
+    nleaf = sum(1 for i in range(nrec) if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE))
     m = re.search(r"// term mode: (\d+) terms", src)
     assert m, "csg32 takes the term form"
     nterms = int(m.group(1))
     assert nterms == 14  # 9 pairs (3 unions of two, 3 differences, 3 lenses) + crater + rounded cube ... as terms
     assert len(re.findall(r"\{  // term: ", src)) == 2 * nterms
     assert "wodev::LdsWindow win" not in src and "WO_EVAL_BEGIN" not in src and "#define WO_JIT_LDS_EVENTS 0" in src
-    nsingle = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|sphere_need|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
-    npair = len(re.findall(r"wodev::axis_pair_meet(_d)?\(", src))
+    nsingle, npair = _leaf_calls(src)
+    assert npair >= 2 * 6  # the slab and the cube
     assert nsingle + 2 * npair == 2 * nleaf
     assert wl.jit_compile_check(src, "gfx950") == ""
     r.close()
@@ -110,10 +117,10 @@ def test_empty_scene_has_no_source(hostonly):
     r.close()
 
 
-def test_member_skip_guards(hostonly, monkeypatch):
+def test_member_skip_guards(hostonly):
     """Members after a primitive's first are guarded by a wave-level emptiness test
-    (scene_jit.c member_skip): one guard per later member in each collect pass, none
-    with WOLOLO_JIT_MEMBER_SKIP=0.  Exact: a met interval only narrows."""
+    (scene_jit.c gen_members): one guard per later member in each collect pass.
+    Exact: a met interval only narrows."""
     guard = "if (__ballot(!(iv.a > iv.b)) != 0ull)"
     r = wl.Renderer("skip", max_nodes=4096)
     scenes.build("csg32", r)
@@ -123,8 +130,6 @@ def test_member_skip_guards(hostonly, monkeypatch):
     singles = len(re.findall(r"wodev::(sphere_interval|sphere_interval_bd|sphere_need|halfspace_interval|halfspace_axis_interval|halfspace_axis_dist)\(", src))
     nprims_emitted = 2 * sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_PRIM)
     assert src.count(guard) == singles + pair_members - nprims_emitted > 0
-    monkeypatch.setenv("WOLOLO_JIT_MEMBER_SKIP", "0")
-    assert guard not in r.jit_source()
     r.close()
 
 
@@ -347,31 +352,27 @@ def _compile_sweep(tmp_path, src, nw, ncull):
     return lib, table != ""
 
 
-@pytest.mark.parametrize("case", ["csg32", "csg256_balanced", "csg256_chain", "chain_uud", "chain_uid",
-                                  "chain_i", "chain_d", "random_a", "random_b", "unionpairs", "unionpairs_s"])
-@pytest.mark.parametrize("knobs", [{}, {"WOLOLO_JIT_DL_EVAL": "0", "WOLOLO_JIT_UNION_COUNT": "0"},
-                                   {"WOLOLO_JIT_UNION_COUNT": "2"}])
-def test_generated_root_evaluation(hostonly, monkeypatch, tmp_path, case, knobs):
-    """The generated root evaluation of the event-list form (WOLOLO_JIT_TERMS=0;
-    flattened literal sets; decision lists for chains, WOLOLO_JIT_DL_EVAL; the
-    incremental count of a union of literal sets, WOLOLO_JIT_UNION_COUNT) compiled on
-    the host is the program's value for random membership words of several densities
-    and for every single primitive, and -- with the union count -- after each of a run
-    of toggles (the sweep's events)."""
+@pytest.mark.parametrize("case", ["csg32_nested", "csg256_balanced", "csg256_chain", "chain_uud", "chain_uid",
+                                  "chain_d", "random_a", "random_b", "unionpairs"])
+def test_generated_root_evaluation(hostonly, tmp_path, case):
+    """The generated root evaluation of the event-list form (the scenes whose root is
+    not a union of small terms: flattened literal sets; decision lists for chains; the
+    incremental count of a union of >= 8 literal-set terms) compiled on the host is the
+    program's value for random membership words of several densities and for every
+    single primitive, and -- with the union count -- after each of a run of toggles
+    (the sweep's events)."""
     import ctypes
 
-    monkeypatch.setenv("WOLOLO_JIT_TERMS", "0")
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
     r = wl.Renderer("eval", max_nodes=4096)
     _build_case(r, case)
     prog, nrec, nprim = r.program()
     src = r.jit_source()
     r.close()
-    if not knobs and case in ("csg256_chain", "chain_uud", "chain_d"):
+    assert "WO_EVAL_BEGIN" in src, case
+    if case in ("csg256_chain", "chain_uud", "chain_d"):
         assert "decision list" in src  # left-deep unions / differences of spheres: one list
         assert wl.jit_compile_check(src, "gfx950") == ""  # and hiprtc takes it
-    if not knobs and case in ("csg256_balanced", "unionpairs"):
+    if case in ("csg256_balanced", "unionpairs"):
         assert "kUTerm" in src  # a union of >= 12 literal-set terms: the incremental count
         assert wl.jit_compile_check(src, "gfx950") == ""
     nw = (nprim + 31) // 32
@@ -410,15 +411,14 @@ def _f32(h):
     return float(np.array([int(h, 16)], dtype=np.uint32).view(np.float32)[0])
 
 
-@pytest.mark.parametrize("case", ["csg32", "csg256_chain", "unionpairs", "random_b"])
-def test_spatial_groups_enclose_their_primitives(hostonly, monkeypatch, case):
+@pytest.mark.parametrize("case", ["csg32_nested", "csg256_chain", "random_a"])
+def test_spatial_groups_enclose_their_primitives(hostonly, case):
     """Spatial collect (scene_jit.c gen_spatial): each wave-level group test's sphere
     (centre and R, R^2 as emitted) encloses the bounding sphere of every primitive the
     group skips when culled, so a culled group never hides a primitive a ray meets;
-    and every primitive is collected exactly once per pass.  (The event-list form:
-    WOLOLO_JIT_TERMS=0; the term form's groups: test_spatial_groups_enclose_their_terms.)"""
-    monkeypatch.setenv("WOLOLO_JIT_TERMS", "0")
-    monkeypatch.setenv("WOLOLO_JIT_SPATIAL", "1")
+    and every primitive is collected exactly once per pass.  (The event-list form over
+    <= 64 primitives or a deep tree; the term form's groups:
+    test_spatial_groups_enclose_their_terms.)"""
     r = wl.Renderer("sp", max_nodes=4096)
     _build_case(r, case)
     prog, nrec, nprim = r.program()
@@ -465,14 +465,13 @@ def test_spatial_groups_enclose_their_primitives(hostonly, monkeypatch, case):
     assert sorted(ords_all) == sorted(list(range(nprim)) * 2)
 
 
-@pytest.mark.parametrize("case", ["csg32", "csg256_balanced", "unionpairs"])
-def test_spatial_groups_enclose_their_terms(hostonly, case, monkeypatch):
-    """The term form groups terms, each bounded by its smallest positive literal's
-    smallest sphere member (a term lies inside each positive literal): every group
-    test's sphere encloses those of the terms it skips when culled, and every
-    primitive is in exactly one term, once per pass.  (Forced: by default the term
-    form is used up to 64 primitives.)"""
-    monkeypatch.setenv("WOLOLO_JIT_TERMS", "1")
+@pytest.mark.parametrize("case", ["csg32", "unionpairs_s"])
+def test_spatial_groups_enclose_their_terms(hostonly, case):
+    """The term form (a root that is a union of <= 2-literal conjunctions over <= 64
+    primitives) groups terms, each bounded by its smallest positive literal's smallest
+    sphere member (a term lies inside each positive literal): every group test's
+    sphere encloses those of the terms it skips when culled, and every primitive is in
+    exactly one term, once per pass."""
     r = wl.Renderer("sp", max_nodes=4096)
     _build_case(r, case)
     prog, nrec, nprim = r.program()

@@ -358,17 +358,6 @@ def test_union_cluster_sah_and_ground_exclusion(hostonly):
     rec.close()
 
 
-def test_union_cluster_without_regrouping_is_the_same_solid(hostonly, monkeypatch):
-    """WOLOLO_REGROUP_UNIONS=0 keeps the scene's own bracketing; both programs describe
-    the node graph's solid."""
-    monkeypatch.setenv("WOLOLO_REGROUP_UNIONS", "0")
-    rec = _big_union_cluster(41)
-    prog, nrec, _ = rec.r.program()
-    P = _sample_points(rec, np.random.default_rng(4), 30000, np.array([-6.5, -6.0, -6.5]), np.array([6.5, 6.0, 6.5]))
-    _check_points(rec, prog, nrec, P)
-    rec.close()
-
-
 def _camera_restated(cam, W, H):
     """RTIOW camera in double precision, written independently of scene_compile.c."""
     look_from, look_at, vup, vfov, aperture, focus = cam

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # bench.py once per (scene, environment) pair; appends "<env> <scene> <ms/frame> <kernel ms>"
-# to gpurun_out/envab.txt.   tools/env_ab.sh "csg32|WOLOLO_JIT_BOUND_MIN_LEAVES=5" ...
+# to gpurun_out/envab.txt.   tools/env_ab.sh "csg32|WOLOLO_JIT_FLAGS=-DWO_LDS_NEXT_EAGER=4" ...
 # A "%" inside a value stands for a space ("WOLOLO_JIT_FLAGS=-mllvm%-opt").
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
