@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--prewarm-s", type=float, default=0.3,
                     help="untimed frames before the warmup steps until this much wall time has passed (clock ramp)")
     ap.add_argument("--scene", default="csg32",
-                    choices=["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain", "csg512_balanced", "csg32_union", "csg256_balanced_union",
+                    choices=["csg32", "csg32_nested", "csg360_nested", "rtiow_cover", "csg256_balanced", "csg256_chain", "csg512_balanced", "csg32_union", "csg256_balanced_union",
                              "sphere256"])
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)

@@ -363,23 +363,33 @@ __device__ __forceinline__ float box_near(float4 lo, float4 hi, F3 ri, F3 oi, fl
 // kMode (PathKind): 2 ordered BVH over union-only primitives, 3 the same over
 // single-sphere primitives only (no generic-primitive code: fewer registers),
 // 6 ordered BVH over the terms of a root that is a union of small conjunctions
-// (extract_terms: the leaves and the always list hold terms), 14 term mode over a
+// (extract_terms: the leaves and the always list hold terms), 7 ordered BVH over
+// the primitives of a general tree (the events in key order, kGWin per walk, and
+// the tree's value kept per lane and updated along the toggled leaf's path), 14 term mode over a
 // 4-wide tree (lb_collapse4: four child boxes per node, half the dependent node
 // loads of a walk; 16-bit stacks) with the resumable walk (trace_step, dynamic
 // ray fetch).  Measured and removed: the general BOUND walk,
 // 16-bit stacks for binary trees, 4-wide trees for primitives, resumable binary
 // walks, a uniform grid and fp16 child boxes.
+// events a general-tree walk collects (the smallest after `after`, sorted)
+#ifndef WO_LANES_GWIN
+#define WO_LANES_GWIN 4
+#endif
+constexpr int kGWin = WO_LANES_GWIN;
+// a general tree's node record (build_lbvh): left ref | right ref << 15 | op << 30
+constexpr uint32_t kGRefBits = 15u, kGRefMask = (1u << kGRefBits) - 1u;
 template <int kModeT, bool kCountT>
 struct LaneTracer {
-    static_assert(kModeT == 2 || kModeT == 3 || kModeT == 6 || kModeT == 14, "lane tracer forms");
+    static_assert(kModeT == 2 || kModeT == 3 || kModeT == 6 || kModeT == 7 || kModeT == 14, "lane tracer forms");
     static constexpr bool kCount = kCountT;
     static constexpr bool kDyn = kModeT == 14;
     static constexpr bool kResumable = kDyn;
     static constexpr int kMode = kModeT;
     static constexpr bool kWide = kMode == 14;
     static constexpr bool kSpheresOnly = kMode == 3;
-    static constexpr bool kStack16 = kWide;
+    static constexpr bool kStack16 = kWide || kMode == 7;
     static constexpr bool kTerms = kMode == 6 || kMode == 14;
+    static constexpr bool kGeneral = kMode == 7;
     static constexpr uint32_t kNodeF4 = kWide ? 7u : 4u;  // float4 per node
     WorkCounts wk;
     uint64_t tmark;  // section timing (counting builds)
@@ -407,6 +417,14 @@ struct LaneTracer {
 #endif
     LdsNodes ltop;
     uint32_t ntop;
+    // general tree (kGeneral): the tree's refs are its leaves (primitive ordinals,
+    // [0, gP)) and internal nodes ([gP, ...)); per lane one bit per ref, the value of
+    // that leaf / node at the current key (a column of gwords words in LDS, [w][lane])
+    uint32_t* gbits;
+    const uint32_t* __restrict__ gpar;   // per ref: its parent's ref, or kNoRef (the root)
+    const uint32_t* __restrict__ gnode;  // per internal node: left | right << 15 | op << 30
+    uint32_t gP, gwords, groot;
+    uint64_t gw[kGWin];  // the walk's smallest event keys after `after`, ascending
 
     // single-sphere scenes: per ordinal its leaf record, then its material (LaneBvh::leaves)
     const WoRec* __restrict__ lleaf;
@@ -581,7 +599,7 @@ struct LaneTracer {
         }
         const uint32_t ord = ref;
 #if WO_LANES_FUSED_SPHERE
-        if constexpr (kSpheresOnly) {
+        if constexpr (kSpheresOnly && !kGeneral) {
             // a sphere's interval [-b - s, -b + s] exists exactly when disc >= 0: the
             // count and the events inside the sqrt branch, no empty interval formed
             // (the specialised kernel's lone spheres; same bits as prim_ivl's form)
@@ -616,6 +634,25 @@ struct LaneTracer {
         }
 #endif
         const Ivl iv = prim_ivl(ord, o, d, inv, have_inv);
+        if constexpr (kGeneral) {
+            if (!(iv.a > iv.b)) {
+                // the first query sets the leaves that hold t_min (the tree's value at
+                // t_min); every query keeps its kGWin smallest keys after `after`, and
+                // prunes with the largest once it has them all
+                if ((after == 0ull) & (iv.a <= tmin) & (iv.b > tmin)) gtoggle(ord);
+                const uint64_t k0 = event_key(iv.a, ord, 0u, iv.ma), k1 = event_key(iv.b, ord, 1u, iv.mb);
+                if ((iv.a > tmin) & (k0 > after)) {
+                    WO_WK(WO_WORK_EVENTS);
+                    ginsert(k0);
+                }
+                if ((iv.b > tmin) & (iv.b < kInf) & (k1 > after)) {
+                    WO_WK(WO_WORK_EVENTS);
+                    ginsert(k1);
+                }
+                best = gw[kGWin - 1];
+            }
+            return;
+        }
         if (!(iv.a > iv.b)) {
             if ((iv.a <= tmin) & (iv.b > tmin)) ++cnt;
             const uint64_t k0 = event_key(iv.a, ord, 0u, iv.ma), k1 = event_key(iv.b, ord, 1u, iv.mb);
@@ -880,7 +917,75 @@ struct LaneTracer {
         }
     }
 
-    __device__ __forceinline__ bool trace(F3 o, F3 d, Hit& hit) { return trace_ordered(o, d, hit); }
+    // ---- general tree (kGeneral) ----
+    __device__ __forceinline__ uint32_t gbit(uint32_t ref) const { return (gbits[(ref >> 5) * kBlock] >> (ref & 31u)) & 1u; }
+    __device__ __forceinline__ void gflip(uint32_t ref) { gbits[(ref >> 5) * kBlock] ^= 1u << (ref & 31u); }
+    // toggle leaf `ord` and re-evaluate its ancestors while their values change
+    __device__ __forceinline__ void gtoggle(uint32_t ord) {
+        WO_WK(WO_WORK_SWEEP_STEPS);
+        uint32_t ref = ord;
+        gflip(ref);
+        for (;;) {
+            const uint32_t par = gpar[ref];
+            if (par == kNoRef) break;  // ref is the root
+            const uint32_t nd = gnode[par - gP];
+            const uint32_t a = gbit(nd & kGRefMask), b = gbit((nd >> kGRefBits) & kGRefMask), op = nd >> 30;
+            const uint32_t v = op == 0u ? (a | b) : op == 1u ? (a & b) : op == 2u ? (a & (b ^ 1u)) : (b & (a ^ 1u));
+            if (v == gbit(par)) break;
+            gflip(par);
+            ref = par;
+        }
+    }
+    __device__ __forceinline__ void ginsert(uint64_t key) {  // the sorted window's insert (Window::insert)
+#pragma unroll
+        for (int i = kGWin - 1; i > 0; --i) gw[i] = key < gw[i - 1] ? gw[i - 1] : (key < gw[i] ? key : gw[i]);
+        gw[0] = key < gw[0] ? key : gw[0];
+    }
+    // Events in key order, kGWin per walk (the walk prunes boxes beyond the largest
+    // once it holds kGWin), each toggling its primitive's leaf; the hit is the first
+    // key at which the root's value differs from its value at t_min -- the general
+    // sweep's hit bit for bit (the tree's value after a key is the program's value of
+    // the leaves' membership there).
+    __device__ __forceinline__ bool trace_general(F3 o, F3 d, Hit& hit) {
+        const float dx = fabsf(d.x) < 1e-30f ? copysignf(1e-30f, d.x) : d.x;
+        const float dy = fabsf(d.y) < 1e-30f ? copysignf(1e-30f, d.y) : d.y;
+        const float dz = fabsf(d.z) < 1e-30f ? copysignf(1e-30f, d.z) : d.z;
+        const F3 ri = f3(__builtin_amdgcn_rcpf(dx), __builtin_amdgcn_rcpf(dy), __builtin_amdgcn_rcpf(dz));
+        const F3 oi = f3(o.x * ri.x, o.y * ri.y, o.z * ri.z);
+        F3 inv = f3(0.0f, 0.0f, 0.0f);
+        bool have_inv = false;
+        for (uint32_t w = 0; w < gwords; ++w) gbits[w * kBlock] = 0u;  // every leaf and node 0
+        uint64_t after = 0ull;
+        uint32_t root0 = 0u;
+        for (;;) {
+#pragma unroll
+            for (int i = 0; i < kGWin; ++i) gw[i] = kEmptyKey;
+            QState s;
+            qbegin(s, after, o, d, inv, have_inv);
+            while (s.cur != kNoRef) trip(s, o, d, ri, oi, inv, have_inv);
+            if (after == 0ull) root0 = gbit(groot);
+#pragma unroll
+            for (int i = 0; i < kGWin; ++i) {
+                const uint64_t key = gw[i];
+                if (key == kEmptyKey) return false;  // every event after `after` processed
+                gtoggle(key_ord(key));
+                const uint32_t rv = gbit(groot);
+                if (rv != root0) {
+                    hit_from_key(key, rv, hit);
+                    return true;
+                }
+            }
+            WO_WK(WO_WORK_RECOLLECTS);
+            after = gw[kGWin - 1];
+        }
+    }
+
+    __device__ __forceinline__ bool trace(F3 o, F3 d, Hit& hit) {
+        if constexpr (kGeneral)
+            return trace_general(o, d, hit);
+        else
+            return trace_ordered(o, d, hit);
+    }
 };
 
 #ifndef WO_LANES_MIN_WAVES
@@ -897,6 +1002,10 @@ struct LaneBvh {
     uint32_t depth;        // internal levels of the tree: the lane stack's entries
     uint32_t ntop;         // nodes [0, ntop) staged in LDS after the lane stacks
     uint32_t dyn_walkers;  // resumable walk: walking lanes at which a wave bails out
+    // general tree (kind 7): parent per ref, node records, leaves, words per lane, root ref
+    const uint32_t* gpar;
+    const uint32_t* gnode;
+    uint32_t gP, gwords, groot;
 };
 
 // Dynamic LDS: the BVH walk's lane stacks ([depth][kBlock] u32 or u16) and top nodes.
@@ -913,7 +1022,11 @@ template <int kMode, bool kCount>
 #ifndef WO_LANES_DYN_TERMS_MIN_WAVES
 #define WO_LANES_DYN_TERMS_MIN_WAVES 6  // csg512_balanced: 56.4 ms at 6 (no spill), 57.2 at 7 (31 VGPRs spilled)
 #endif
+#ifndef WO_LANES_GENERAL_MIN_WAVES
+#define WO_LANES_GENERAL_MIN_WAVES 4  // the tree's bits take ~20 KB of LDS per workgroup (csg360_nested)
+#endif
 __global__ __launch_bounds__(kBlock, kMode == 14  ? WO_LANES_DYN_TERMS_MIN_WAVES
+                                    : kMode == 7 ? WO_LANES_GENERAL_MIN_WAVES
                                     : kMode == 6 ? WO_LANES_TERMS_MIN_WAVES
                                     : kMode == 2 ? WO_LANES_BVH_MIN_WAVES
                                                  : WO_LANES_MIN_WAVES) void pathtrace_lanes_kernel(
@@ -950,6 +1063,15 @@ __global__ __launch_bounds__(kBlock, kMode == 14  ? WO_LANES_DYN_TERMS_MIN_WAVES
         for (uint32_t i = threadIdx.x; i < kNodeF4 * bvh.ntop; i += kBlock) top[i] = bvh.nodes[i];
         tr.ltop = (typename LaneTracer<kMode, kCount>::LdsNodes)top;
         tr.ntop = bvh.ntop;
+        if constexpr (LaneTracer<kMode, kCount>::kGeneral) {
+            // the tree's bits after the top nodes, [word][lane]
+            tr.gbits = reinterpret_cast<uint32_t*>(top + kNodeF4 * bvh.ntop) + threadIdx.x;
+            tr.gpar = bvh.gpar;
+            tr.gnode = bvh.gnode;
+            tr.gP = bvh.gP;
+            tr.gwords = bvh.gwords;
+            tr.groot = bvh.groot;
+        }
     }
     pathtrace_block(tr, mats, fr, local_rows, out, seg_slots, tg);
 }
@@ -1216,6 +1338,9 @@ struct WoDev {
     bool lb_stack16;       // 16-bit stack entries (the 4-wide tree)
     bool lb_wide;          // 4-wide nodes of 7 float4 (lb_collapse4; kind 14)
     uint32_t lb_terms;     // term mode (kinds 6 / 14): terms the BVH's leaves and always list refer to
+    bool lb_general;       // a general tree (kind 7): the BVH over primitives, the tree's tables below
+    uint32_t lb_gpar_off, lb_gnode_off;  // u32 offsets in d_lbvh of the parent per ref / node records
+    uint32_t lb_gP, lb_gwords, lb_groot;  // leaves (= primitives), bit words per lane, the root's ref
     uint32_t last_kind;    // the PathKind of the last path launch (wo_dev_lanes_info)
     uint32_t lb_term_off;  // their records (kTermRecF4 float4 each) at this u32 offset of d_lbvh
     uint32_t lb_leaf_off;  // single-sphere scenes: per ordinal its leaf record (WoRec) at this u32 offset, else 0
@@ -1768,10 +1893,47 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     dev->lb_stack16 = false;
     dev->lb_wide = false;
     dev->lb_terms = 0;
+    dev->lb_general = false;
     // not union-only: the BVH over the root's terms, when the root is a union of
-    // small conjunctions (extract_terms)
+    // small conjunctions (extract_terms); else over the primitives of the general tree,
+    // whose value the lanes keep (gpar / gnode: the tree over the primitives, BOUND
+    // records dropped; refs [0, P) the primitives' leaves, [P, P + nodes) the binops)
     std::vector<std::vector<uint32_t>> terms;
-    if (!dev->union_only && !extract_terms(prog, n_recs, n_prims, terms)) return 0;
+    std::vector<uint32_t> gpar, gnode;
+    uint32_t groot = kNoRef;
+    if (!dev->union_only && !extract_terms(prog, n_recs, n_prims, terms)) {
+        if (!n_prims) return 0;
+        gpar.assign(n_prims, kNoRef);
+        std::vector<uint32_t> st;
+        for (uint32_t pc = 0; pc < n_recs;) {
+            const WoRec& r = prog[pc];
+            if (r.op == WO_OP_PRIM) {
+                st.push_back(r.u1);
+                pc += 1u + r.u0;
+                continue;
+            }
+            ++pc;
+            if (r.op == WO_OP_BOUND) continue;
+            if (st.size() < 2u) {
+                snprintf(err, errlen, "malformed program (binop without operands)");
+                return -1;
+            }
+            const uint32_t b = st.back();
+            st.pop_back();
+            const uint32_t a = st.back();
+            st.pop_back();
+            const uint32_t op = r.op == WO_OP_UNION ? 0u : r.op == WO_OP_INTER ? 1u : r.op == WO_OP_DIFF ? 2u : 3u;
+            const uint32_t n = n_prims + (uint32_t)gnode.size();
+            gnode.push_back(a | (b << kGRefBits) | (op << 30));
+            gpar.push_back(kNoRef);
+            gpar[a] = n;
+            gpar[b] = n;
+            st.push_back(n);
+        }
+        if (st.size() != 1u || gpar.size() > kGRefMask) return 0;  // (refs beyond 15 bits: no lane form)
+        groot = st[0];
+        dev->lb_general = true;
+    }
     std::vector<LbPrim> prims;
     std::vector<uint32_t> always;
     std::vector<float4> geo(n_prims, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
@@ -1959,17 +2121,24 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     dev->lb_nodes = (uint32_t)(nodes.size() / node_f4);
     dev->lb_always = (uint32_t)always.size();
     {
-        // 16-bit stack entries for 4-wide nodes (binary trees: 32-bit, RTIOW cover
-        // 11.60 ms against 11.76 with 16-bit entries and more top nodes)
-        dev->lb_stack16 = dev->lb_wide;
+        // 16-bit stack entries for 4-wide nodes and the general tree (its bits need the
+        // LDS; binary trees otherwise: 32-bit, RTIOW cover 11.60 ms against 11.76 with
+        // 16-bit entries and more top nodes)
+        dev->lb_stack16 = dev->lb_wide || dev->lb_general;
+        if (dev->lb_general && (dev->lb_nodes >= 0x8000u || n_prims >= 0x8000u)) {
+            dev->lb_general = false;  // refs beyond the 16-bit stack entries: no lane form
+            return 0;
+        }
         // the top nodes fill what the stacks leave of kLanesBvhLds (8 workgroups per CU)
         const size_t stacks =
             ((((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u)) + 15u) & ~(size_t)15u);
+        const size_t used = stacks + (dev->lb_general ? (size_t)((gpar.size() + 31u) / 32u) * kBlock * 4u : 0u);
         const uint32_t top =
-            stacks < kLanesBvhLds ? (uint32_t)((kLanesBvhLds - stacks) / (node_f4 * sizeof(float4))) : 0u;
+            used < kLanesBvhLds ? (uint32_t)((kLanesBvhLds - used) / (node_f4 * sizeof(float4))) : 0u;
         dev->lb_top = top < dev->lb_nodes ? top : dev->lb_nodes;
     }
-    dev->lb_spheres_only = terms.empty() && std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
+    dev->lb_spheres_only = terms.empty() && !dev->lb_general &&
+                           std::all_of(kind.begin(), kind.end(), [](uint32_t k) { return k != 0u; });
     dev->lb_terms = (uint32_t)terms.size();
     const size_t f4 = nodes.size() + n_prims;
     // ... | kind per ordinal | always list | (term mode) kTermRecF4 float4 per term, 16-byte aligned
@@ -1983,9 +2152,18 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     static_assert(sizeof(WoRec) == 32 && sizeof(WoMaterial) == 32, "leaf table entries are 2 x 32 bytes");
     const size_t leaf_off = term_off + term_recs.size() * sizeof(float4);
     dev->lb_leaf_off = dev->lb_spheres_only ? (uint32_t)(leaf_off / sizeof(uint32_t)) : 0u;
-    const size_t bytes = leaf_off + (dev->lb_spheres_only ? (size_t)n_prims * 2u * sizeof(WoRec) : 0u);
+    const size_t gpar_off = leaf_off + (dev->lb_spheres_only ? (size_t)n_prims * 2u * sizeof(WoRec) : 0u);
+    const size_t gnode_off = gpar_off + gpar.size() * sizeof(uint32_t);
+    const size_t bytes = gnode_off + gnode.size() * sizeof(uint32_t);
+    dev->lb_gpar_off = (uint32_t)(gpar_off / sizeof(uint32_t));
+    dev->lb_gnode_off = (uint32_t)(gnode_off / sizeof(uint32_t));
+    dev->lb_gP = n_prims;
+    dev->lb_gwords = (uint32_t)((gpar.size() + 31u) / 32u);
+    dev->lb_groot = groot;
     if (ensure_buffer(&dev->d_lbvh, &dev->lbvh_cap, bytes, err, errlen)) return -1;
     std::vector<char> blob(bytes);
+    if (!gpar.empty()) memcpy(blob.data() + gpar_off, gpar.data(), gpar.size() * sizeof(uint32_t));
+    if (!gnode.empty()) memcpy(blob.data() + gnode_off, gnode.data(), gnode.size() * sizeof(uint32_t));
     if (dev->lb_spheres_only)
         for (uint32_t ord = 0; ord < n_prims; ++ord) {
             const WoRec& L = prog[pc_of[ord] + 1u];
@@ -2025,6 +2203,11 @@ static LaneBvh lane_bvh(const WoDev* dev) {
     b.leaves = dev->lb_leaf_off ? reinterpret_cast<const WoRec*>(reinterpret_cast<const uint32_t*>(dev->d_lbvh) +
                                                                 dev->lb_leaf_off)
                                 : nullptr;
+    b.gpar = reinterpret_cast<const uint32_t*>(dev->d_lbvh) + dev->lb_gpar_off;
+    b.gnode = reinterpret_cast<const uint32_t*>(dev->d_lbvh) + dev->lb_gnode_off;
+    b.gP = dev->lb_gP;
+    b.gwords = dev->lb_gwords;
+    b.groot = dev->lb_groot;
     return b;
 }
 
@@ -2079,11 +2262,14 @@ struct JitEntry {
     uint64_t used;
 };
 static const size_t kJitCacheEntries = 8;
-static std::mutex g_jit_mu;
+// The process cache and its lock live on the heap and are never destroyed: a
+// background compile still running when the process exits (a renderer never
+// closed) then touches no destroyed static.
+static std::mutex& g_jit_mu = *new std::mutex;
 static uint64_t g_jit_tick;
 static std::unordered_map<std::string, JitEntry>& jit_cache() {
-    static std::unordered_map<std::string, JitEntry> m;
-    return m;
+    static auto* m = new std::unordered_map<std::string, JitEntry>;
+    return *m;
 }
 static void jit_cache_put(const std::string& key, const std::vector<char>& code) {  // g_jit_mu held
     auto& m = jit_cache();
@@ -2374,7 +2560,7 @@ extern "C" int wo_jit_compile_check(const char* src, const char* arch, char* err
 
 extern "C" int wo_dev_jit_active(WoDev* dev) { return dev && dev->jit_fn ? 1 : 0; }
 extern "C" int wo_dev_lanes_available(WoDev* dev) {
-    return dev && (dev->union_only || dev->lb_terms) ? 1 : 0;
+    return dev && (dev->union_only || dev->lb_terms || dev->lb_general) ? 1 : 0;
 }
 extern "C" void wo_dev_set_lanes(WoDev* dev, int on) {
     if (dev) dev->lanes_on = on != 0;
@@ -2455,8 +2641,8 @@ extern "C" int wo_dev_launch(WoDev* dev, WoFrame const* frame_in, void* d_out, v
 }
 
 // the numbers are wo_renderer_lanes_info's "kind" (the lane tracer's forms, LaneTracer)
-enum PathKind { kLanesBvh = 2, kLanesBvhSpheres = 3, kLanesTerms = 6, kLanesDynWideTerms = 14, kJit = 16, kInterpLds = 17,
-                kInterpGlobal = 18 };
+enum PathKind { kLanesBvh = 2, kLanesBvhSpheres = 3, kLanesTerms = 6, kLanesGeneral = 7, kLanesDynWideTerms = 14,
+                kJit = 16, kInterpLds = 17, kInterpGlobal = 18 };
 
 template <bool kCount>
 static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
@@ -2467,6 +2653,8 @@ static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<3, kCount>, kBlock, dyn_lds);
     case kLanesTerms:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<6, kCount>, kBlock, dyn_lds);
+    case kLanesGeneral:
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<7, kCount>, kBlock, dyn_lds);
     case kLanesDynWideTerms:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_lanes_kernel<14, kCount>, kBlock, dyn_lds);
     case kInterpLds:
@@ -2496,6 +2684,9 @@ static void static_launch(PathKind kind, dim3 grid, size_t dyn_lds, hipStream_t 
         break;
     case kLanesTerms:
         lanes_launch<6, kCount>(grid, dyn_lds, stream, dev, fr, local_rows, out, slots, tg);
+        break;
+    case kLanesGeneral:
+        lanes_launch<7, kCount>(grid, dyn_lds, stream, dev, fr, local_rows, out, slots, tg);
         break;
     case kLanesDynWideTerms:
         lanes_launch<14, kCount>(grid, dyn_lds, stream, dev, fr, local_rows, out, slots, tg);
@@ -2573,17 +2764,19 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
         PathKind kind;
         size_t dyn_lds = 0;
         KLayout lay = {};
-        if (dev->lanes_on && (dev->union_only || dev->lb_terms) && !dev->jit_fn) {
+        if (dev->lanes_on && (dev->union_only || dev->lb_terms || dev->lb_general) && !dev->jit_fn) {
             // the ordered BVH, its lane stacks and top nodes in LDS.  Term mode over more
             // than 256 terms: the 4-wide tree with the resumable walk (dynamic ray fetch;
             // csg512_balanced 84.3 -> 44.7 ms; slower where walks are short or alike: the
             // RTIOW cover 11.7 -> 12.9-15.5 ms, csg256 balanced's 65 terms 16.5 -> 18.2;
             // DESIGN.md §3.6c)
-            kind = dev->lb_wide ? kLanesDynWideTerms
-                   : dev->lb_terms ? kLanesTerms
+            kind = dev->lb_wide      ? kLanesDynWideTerms
+                   : dev->lb_terms   ? kLanesTerms
+                   : dev->lb_general ? kLanesGeneral
                    : (dev->lb_spheres_only ? kLanesBvhSpheres : kLanesBvh);
             const size_t stacks = ((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u) + 15u) & ~(size_t)15u;
             dyn_lds = stacks + (size_t)dev->lb_top * lb_node_f4(dev) * sizeof(float4);
+            if (dev->lb_general) dyn_lds += (size_t)dev->lb_gwords * kBlock * sizeof(uint32_t);  // the tree's bits
         } else if (dev->jit_fn) {
             kind = kJit;
         } else {

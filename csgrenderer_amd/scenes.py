@@ -264,7 +264,8 @@ class NestedShape:
 _NESTED_OPS = "dui"
 
 
-def build_csg32_nested(r: Renderer, seed: int = 3235, width=1920, height=1080, spp=64, mirror=None) -> SceneInfo:
+def build_csg32_nested(r: Renderer, seed: int = 3235, width=1920, height=1080, spp=64, mirror=None,
+                       items: int = 22, boxes=(6, 17)) -> SceneInfo:
     """C3 as SURVEY.md §8(d) wrote it: 32 leaves (20 spheres + 12 half-spaces forming two
     6-plane boxes) in ONE balanced tree with intersections and differences at every
     level (31 binops, 63 nodes) -- unlike csg32, whose root is a union of small terms
@@ -275,10 +276,13 @@ def build_csg32_nested(r: Renderer, seed: int = 3235, width=1920, height=1080, s
     of their size, a difference bites a smaller operand out of the side of a larger
     one.  tests/test_scenes.py checks on sampled points that every intersection and
     every difference of the built tree is non-empty and that every difference removes
-    something.  `mirror` (a list) receives the tree's NestedShape."""
+    something.  `mirror` (a list) receives the tree's NestedShape.
+
+    `items` / `boxes`: the same construction over more leaves (csg360_nested: 337
+    spheres and 23 boxes, 474 binops, 309 primitives -- the > 256-primitive general tree)."""
     rng = Pcg32(seed)
-    n_items = 22  # 20 spheres + 2 boxes (a box is a chain of 6 half-space intersections)
-    box_at = {6, 17}
+    n_items = items  # csg32_nested: 20 spheres + 2 boxes (a box is a chain of 6 half-space intersections)
+    box_at = set(boxes)
     pos_at_depth = {}
     leaf_no = [0]
 
@@ -296,7 +300,7 @@ def build_csg32_nested(r: Renderer, seed: int = 3235, width=1920, height=1080, s
             if k in box_at:
                 half = (0.8 * rad, 0.55 * rad, 0.8 * rad)
                 node, planes = _box_extents(r, centre, half)
-                m = r.metal((0.8, 0.85, 0.9), 0.05) if k == 6 else r.lambertian((0.3, 0.5, 0.7))
+                m = r.metal((0.8, 0.85, 0.9), 0.05) if k % 2 == 0 else r.lambertian((0.3, 0.5, 0.7))
                 for pl in planes:
                     r.set_material(pl, m)
                 return (node, (0.0, 0.0, 0.0)), NestedShape("box", centre=centre, size=half)
@@ -324,8 +328,10 @@ def build_csg32_nested(r: Renderer, seed: int = 3235, width=1920, height=1080, s
     if mirror is not None:
         mirror.append(shape)
     r.set_camera((0.0, 2.4, 6.0), (0.0, 1.4, 0.0), (0, 1, 0), 38.0, 0.0, 6.0)
-    return SceneInfo("csg32_nested", spheres=20, halfspaces=12, binops=31, width=width, height=height, spp=spp,
-                     max_depth=8)
+    nb = len(box_at)
+    name = "csg32_nested" if n_items == 22 else f"csg{n_items}_nested"
+    return SceneInfo(name, spheres=n_items - nb, halfspaces=6 * nb, binops=n_items - 1 + 5 * nb, width=width,
+                     height=height, spp=spp, max_depth=8)
 
 
 def build_csg256(r: Renderer, seed: int = 256, shape: str = "balanced", width=1920, height=1080,
@@ -381,6 +387,10 @@ SCENES = {
     # scene (512 sphere leaves: 255 overlapping pairs + ground + glass ball, 427
     # primitives) -- not a BASELINE config, the measure of the >256-primitive path
     "csg512_balanced": lambda r, **k: build_csg256(r, shape="balanced", pairs=255, **k),
+    # csg32_nested's construction over 360 items (337 spheres, 23 boxes: 475 leaves, 309
+    # primitives): a general tree (intersections and differences at every level) of more
+    # than 256 primitives -- not a BASELINE config, the measure of that path
+    "csg360_nested": lambda r, **k: build_csg32_nested(r, items=360, boxes=range(7, 360, 16), **k),
 }
 
 

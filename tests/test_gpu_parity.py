@@ -130,7 +130,9 @@ def _union_of_terms(r, max_lits=2):
 
 
 def _lanes_eligible(r):
-    return _union_only(r) or _union_of_terms(r)
+    """The lane tracer takes every scene: union-only (a count), a union of small terms
+    (term mode), else the general tree (its value kept per lane, kind 7)."""
+    return r.program()[2] > 0
 
 
 def _check_path(r, path, scene=None):
@@ -140,7 +142,7 @@ def _check_path(r, path, scene=None):
         want = "interpreter"
     elif path == "lanes" and _lanes_eligible(r):
         want = "lanes"
-    else:  # JIT up to WOLOLO_JIT_MAX_PRIMS (256) primitives; above, the lanes where they apply (rtiow_cover's 487)
+    else:  # JIT up to WOLOLO_JIT_MAX_PRIMS (256) primitives; above, the lanes (rtiow_cover's 487, csg360_nested's 309)
         want = "jit" if 0 < nprim <= 256 else ("lanes" if _lanes_eligible(r) else "interpreter")
     assert r.trace_path() == want, (scene, r.trace_path(), want)
 
@@ -155,11 +157,12 @@ def _oracle_rows(r, params):
 
 @pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("scene", ["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain",
-                                   "csg512_balanced"])
+                                   "csg512_balanced", "csg360_nested"])
 @pytest.mark.parametrize("mode", [wl.MODE_PATHTRACE, wl.MODE_NORMALS])
 def test_pathtrace_small_frame_bitexact(scene, mode, path):
     r, info = _scene(scene, path)
-    p = info.params(width=96, height=54, spp=8 if mode == wl.MODE_PATHTRACE else 1, mode=mode, seed=7)
+    w, h, spp = (48, 27, 4) if scene == "csg360_nested" else (96, 54, 8)  # the oracle's cost: every leaf, every event
+    p = info.params(width=w, height=h, spp=spp if mode == wl.MODE_PATHTRACE else 1, mode=mode, seed=7)
     img = r.render(p)
     _check_path(r, path, scene)
     ref, _ = _oracle_rows(r, p)
@@ -169,15 +172,13 @@ def test_pathtrace_small_frame_bitexact(scene, mode, path):
 
 @pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("scene", ["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain",
-                                   "csg512_balanced"])
+                                   "csg512_balanced", "csg360_nested"])
 def test_pathtrace_full_size_sampled_pixels(scene, path):
     """BASELINE configs at full size (1920x1080, 64 spp, 8 bounces): the whole frame on
-    the GPU, a random sample of pixels on the oracle.  The lane tracer runs union-only
-    scenes only (elsewhere the setting falls back to the JIT, which its own case covers)."""
+    the GPU, a random sample of pixels on the oracle.  Every path runs every scene (the
+    lane tracer's general form takes the trees that are neither union-only nor a union
+    of small terms)."""
     r, info = _scene(scene, path)
-    if path == "lanes" and not _lanes_eligible(r):
-        r.close()
-        pytest.skip("lanes: not a union of small terms (the tracer falls back to the jit case)")
     p = info.params()
     img = r.render(p)
     _check_path(r, path, scene)
@@ -474,19 +475,21 @@ def test_lanes_bvh_depth_bound(monkeypatch):
 # the lane tracer's form per scene (PathKind: 2 generic primitives, 3 single spheres,
 # 6 term mode over <= 256 terms, 14 the resumable 4-wide term-mode walk)
 _LANE_KIND = {"union90": 2, "rtiow_cover": 3, "deep600": 3, "glass200": 3, "csg32": 6, "csg256_balanced": 6,
-              "csg512_balanced": 14}
+              "csg512_balanced": 14, "csg32_nested": 7, "csg256_chain": 7, "csg360_nested": 7}
 
 
 @pytest.mark.parametrize("scene", ["union90", "rtiow_cover", "csg32", "csg256_balanced", "deep600", "glass200",
-                                   "csg512_balanced"])
+                                   "csg512_balanced", "csg32_nested", "csg256_chain", "csg360_nested"])
 def test_lane_tracer_forms_bitexact(scene, monkeypatch):
     """Every form of the lane tracer, each on the scenes that take it: the binary walk
     over generic primitives (boxes, half-spaces: the union scene), over single spheres
     (the RTIOW cover; the 600-sphere chain whose tree is as deep as the depth bound
     allows; a cluster of overlapping glass spheres, rays that start inside), term mode
-    over <= 256 terms (csg32, csg256 balanced) and the resumable 4-wide term-mode walk
+    over <= 256 terms (csg32, csg256 balanced), the resumable 4-wide term-mode walk
     (csg512_balanced: a wave's walking lanes bail out once few lanes walk, the others
-    shade and fetch new rays); every image the oracle's bit for bit."""
+    shade and fetch new rays) and the general tree (csg32_nested, the csg256 chain,
+    csg360_nested: events in key order, the tree's value kept per lane); every image
+    the oracle's bit for bit."""
     monkeypatch.setenv("WOLOLO_LANES_MIN_PRIMS", "64")
     if scene == "union90":
         r = _union_scene()
@@ -522,7 +525,8 @@ def test_lane_tracer_forms_bitexact(scene, monkeypatch):
         p = wl.render_params(64, 48, spp=4, max_depth=8, mode=wl.MODE_PATHTRACE, seed=5)
     else:
         r, info = _scene(scene, "lanes")
-        p = info.params(width=96, height=54, spp=8, seed=7)
+        p = info.params(width=48, height=27, spp=4, seed=7) if scene == "csg360_nested" else \
+            info.params(width=96, height=54, spp=8, seed=7)
     r.set_tracer("lanes")
     for mode in (wl.MODE_NORMALS, wl.MODE_PATHTRACE):
         p.mode = mode
@@ -540,9 +544,10 @@ def test_lane_tracer_forms_bitexact(scene, monkeypatch):
 def test_auto_tracer_choices():
     """AUTO: the RTIOW cover (union-only, 487 primitives) takes the lane tracer; csg32 and a
     128-primitive union-only scene the JIT; csg512_balanced (427 primitives, a union of
-    small terms) the lane tracer's resumable 4-wide term-mode walk."""
+    small terms) the lane tracer's resumable 4-wide term-mode walk; csg360_nested (309
+    primitives of a general tree) its general form."""
     for name, want in [("rtiow_cover", "lanes"), ("csg32", "jit"), ("csg256_balanced_union", "jit"),
-                       ("csg512_balanced", "lanes")]:
+                       ("csg512_balanced", "lanes"), ("csg360_nested", "lanes")]:
         r, info = _scene(name, "auto")
         r.render(info.params(width=32, height=18, spp=1))
         assert r.trace_path() == want, (name, r.trace_path())
@@ -551,6 +556,9 @@ def test_auto_tracer_choices():
         if name == "csg512_balanced":
             # > 256 terms: the resumable 4-wide walk in term mode (kLanesDynWideTerms)
             assert r.lanes_info()["kind"] == 14, r.lanes_info()
+        if name == "csg360_nested":
+            # > 256 primitives of a general tree: kLanesGeneral
+            assert r.lanes_info()["kind"] == 7, r.lanes_info()
         r.close()
 
 

@@ -15,6 +15,10 @@ frame, on rank 0's GPU:
     assemble stream: after the copies, assemble_kernel into the frame + the sRGB
                      encode (with --no-encode: the bench's frame, which is not
                      presented)
+    map-back stream: after the encode, the present encode's D2H into pinned host
+                     memory (--map-back bgra, draw_frame's default; `float` adds the
+                     float frame, `none` skips it) -- wo_renderer_draw_frame's copy
+                     stream
 
 two frames in flight (two gather buffers, two render streams), F frames back to back.
 Every other rank's step is its share alone, timed the same way (back to back over two
@@ -44,6 +48,8 @@ def main():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--no-encode", action="store_true")
     ap.add_argument("--tile-rows", type=int, default=4, help="rows per row-cyclic band (bench.py --tile-rows)")
+    ap.add_argument("--map-back", default="bgra", choices=["bgra", "float", "none"],
+                    help="rank 0's D2H of the presented frame after the encode (draw_frame: bgra)")
     args = ap.parse_args()
 
     import torch
@@ -83,12 +89,16 @@ def main():
     t1 = timed(one_gpu)
     print(f"[root] N=1 {t1:.3f} ms per frame", flush=True)
     res = {"scene": args.scene, "size": f"{W}x{H}x{p.spp}", "path": r.trace_path(), "one_gpu_ms": round(t1, 4),
-           "encode": not args.no_encode, "worlds": {}}
+           "encode": not args.no_encode, "map_back": "none" if args.no_encode else args.map_back, "worlds": {}}
+    mapback = not args.no_encode and args.map_back != "none"
+    hb = [torch.empty((H, W), dtype=torch.int32).pin_memory() for _ in range(2)] if mapback else []
+    hf = [torch.empty((H, W, 4), dtype=torch.float32).pin_memory() for _ in range(2)] \
+        if mapback and args.map_back == "float" else []
     for n in args.worlds:
         lr = wl.local_rows(H, T, n)
         share_bytes = lr * W * 16
         rs = [torch.cuda.Stream(), torch.cuda.Stream()]
-        cps, asm = torch.cuda.Stream(), torch.cuda.Stream()
+        cps, asm, d2h = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
         gather = [torch.empty((n, lr, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
         frames = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
         bgra = [torch.empty((H, W), dtype=torch.int32, device="cuda") for _ in range(2)]
@@ -105,9 +115,10 @@ def main():
             return go
 
         def root(start):
-            for st in rs + [cps, asm]:
+            for st in rs + [cps, asm, d2h]:
                 st.wait_event(start)
             released = [None, None]
+            mapped = [None, None]  # the D2H that last read the slot's encode / frame
             for k in range(F):
                 b = k & 1
                 if released[b] is not None:
@@ -122,13 +133,24 @@ def main():
                 copied = torch.cuda.Event()
                 copied.record(cps)
                 asm.wait_event(copied)
+                if mapped[b] is not None:
+                    asm.wait_event(mapped[b])
                 wl.assemble_rows_device(gather[b].data_ptr(), frames[b].data_ptr(), W, H, T, n, asm.cuda_stream)
                 if not args.no_encode:
                     wl.srgb8_encode_device(frames[b].data_ptr(), bgra[b].data_ptr(), W * H, asm.cuda_stream)
                 ev = torch.cuda.Event()
                 ev.record(asm)
                 released[b] = ev
-            for st in rs + [cps, asm]:
+                if mapback:
+                    d2h.wait_event(ev)
+                    with torch.cuda.stream(d2h):
+                        hb[b].copy_(bgra[b], non_blocking=True)
+                        if hf:
+                            hf[b].copy_(frames[b], non_blocking=True)
+                    mev = torch.cuda.Event()
+                    mev.record(d2h)
+                    mapped[b] = mev
+            for st in rs + [cps, asm, d2h]:
                 main_s.wait_stream(st)
 
         root(torch.cuda.Event())  # first use of the streams and buffers, untimed
@@ -141,7 +163,8 @@ def main():
                             "share_bytes": share_bytes, "projected_frame_ms": round(proj, 4),
                             "projected_speedup": round(t1 / proj, 3)}
         print(f"[root] N={n} rank 0 step {root_ms:.3f} ms (share + {n - 1} copies of {share_bytes / 1e6:.1f} MB "
-              f"+ assemble{'' if args.no_encode else ' + encode'}), slowest other share {worst_other:.3f} ms "
+              f"+ assemble{'' if args.no_encode else ' + encode'}{' + D2H ' + args.map_back if mapback else ''}), "
+              f"slowest other share {worst_other:.3f} ms "
               f"-> {proj:.3f} ms per frame, {t1 / proj:.2f}x", flush=True)
     print(json.dumps(res))
     r.close()
