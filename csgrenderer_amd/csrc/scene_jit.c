@@ -1276,7 +1276,6 @@ static void gen_union_sweep(Gen* g, const UTerm* uterms, uint32_t n_uterms, uint
     gen_collect_all(g, 10);
     bput(b,
          "        }\n"
-         "        win.seal();\n"
          "        if (!win.next(key)) return false;\n"
          "      }\n"
          "      WO_WK(WO_WORK_SWEEP_STEPS);\n"
@@ -1525,14 +1524,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * LDS within the CU (csg32 5.24 -> 5.19 ms; csg256 balanced keeps 8 entries:
      * 15.12 vs 15.33 ms at 7) */
     if (g.lds_events && n_prims <= 64u) bput(&b, "#ifndef WO_LDS_EVENTS\n#define WO_LDS_EVENTS 7\n#endif\n");
-    /* a general root evaluation sweeps many events per segment (csg32_nested
-     * 4.5): its LDS list is sorted once per collect (SortedLdsWindow) */
-    const int sorted_win = g.lds_events && !n_uterms && !g.term_mode;
-    bput(&b, "#ifndef WO_SORTED_EVENTS\n#define WO_SORTED_EVENTS %d\n#endif\n", sorted_win);
-    bput(&b, "#include \"wo_device_common.h\"\n"
-             "#if WO_SORTED_EVENTS\n#define WO_SORTED_WINDOW wodev::SortedLdsWindow\n"
-             "#else\n#define WO_SORTED_WINDOW wodev::LdsWindow\n#endif\n"
-             "#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
+    bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
          g.lds_events && !g.term_mode, tree_depth(prog, n_recs), lds_prog);
     if (n_uterms) {
         bput(&b, "struct __attribute__((aligned(16))) WoUTerm { uint64_t m, q; uint32_t w, neg, pad0, pad1; };\n");
@@ -1639,7 +1631,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "    uint64_t after = 0ull, key = 0ull;\n"
              "    WO_MARK(\"collect_begin\");\n"
              "    {\n",
-             !g.lds_events ? "wodev::Window" : sorted_win ? "WO_SORTED_WINDOW" : "wodev::LdsWindow",
+             !g.lds_events ? "wodev::Window" : "wodev::LdsWindow",
              !g.lds_events ? "" : "win.ev = ev; ");
         g.first_pass = 1;
         gen_collect_all(&g, 6);
@@ -1647,7 +1639,6 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
              "    }\n"
              "    WO_MARK(\"collect_end\");\n"
              "    WO_TMARK();\n"
-             "    win.seal();\n"
              "    if (win.empty()) return false;\n"
              "    bool have = false;\n"
              "    uint32_t root = 0u;\n");
@@ -1714,7 +1705,6 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             gen_collect_all(&g, 10);
             bput(&b,
                  "        }\n"
-                 "        win.seal();\n"
                  "        if (!win.next(key)) return false;\n"
                  "      }\n"
                  "      have = true;\n"

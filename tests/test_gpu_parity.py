@@ -586,7 +586,6 @@ def test_jit_event_windows(window, monkeypatch):
     "-DWO_LDS_EVENTS=2 -DWO_LDS_NEXT_EAGER=7",  # eager reads clamped to the list
     "-DWO_LDS_KEEP_SMALLEST=0",  # a full event list keeps its first keys
     "-DWO_LDS_EVENTS=3",  # ... or its 3 smallest (overflow on most nested rays)
-    "-DWO_SORTED_EVENTS=0",  # csg32_nested's list scanned per event instead of sorted once
 ])
 def test_jit_compile_flag_variants(flags, monkeypatch):
     """The event list's compile-time variants (WOLOLO_JIT_FLAGS) change how much work a

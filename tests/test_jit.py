@@ -67,7 +67,7 @@ def test_generated_sources_compile_for_gfx950(hostonly):
     naxis = sum(1 for i in range(nrec) if prog[i].op == wl.WO_LEAF_HALFSPACE and prog[i].u1 != 0)
     assert naxis >= 12
     assert len(re.findall(r"wodev::halfspace_axis_(interval|dist)\(", src)) + 2 * npair == 2 * naxis
-    assert "#define WO_SORTED_EVENTS 1" in src and "WO_EVAL_BEGIN" in src  # the sorted event list, a general root
+    assert "wodev::LdsWindow win" in src and "WO_EVAL_BEGIN" in src  # the LDS event list, a general root
     assert wl.jit_compile_check(src, "gfx950") == ""
     r.close()
     # the term form (the root is a union of <= 2-literal conjunctions): every leaf still
