@@ -549,6 +549,14 @@ typedef struct JTSub {
     uint32_t start, count;
 } JTSub;
 
+/* Key constants of primitive `ord` as a term literal of polarity `pos`: the rise
+ * flag (bit 10) on the event where the literal becomes true -- wodev::term_ka /
+ * term_kb; JIT_TERM_MAX_MEMBERS = wodev::kTermMaxMembers. */
+#define JIT_TERM_RISE (1u << 10)
+#define JIT_TERM_MAX_MEMBERS JIT_TERM_RISE
+static uint32_t term_ka(uint32_t ord, int pos) { return (ord << 12) | (pos ? JIT_TERM_RISE : 0u); }
+static uint32_t term_kb(uint32_t ord, int pos) { return (ord << 12) | (1u << 11) | (pos ? 0u : JIT_TERM_RISE); }
+
 /* The root's terms (malloc'd, *nt of them), or NULL when the root is not a union of
  * such conjunctions. */
 static JTerm* jit_terms(const WoRec* prog, uint32_t n_recs, uint32_t n_prims, uint32_t* nt) {
@@ -559,6 +567,10 @@ static JTerm* jit_terms(const WoRec* prog, uint32_t n_recs, uint32_t n_prims, ui
     for (uint32_t pc = 0; pc < n_recs && ok;) {
         const WoRec* r = &prog[pc];
         if (r->op == WO_OP_PRIM) {
+            if (r->u0 >= JIT_TERM_MAX_MEMBERS) { /* its member index would reach the rise flag */
+                ok = 0;
+                break;
+            }
             JTSub x;
             memset(&x, 0, sizeof x);
             x.t.n = 1;
@@ -647,7 +659,7 @@ static void gen_term_ivl(Gen* g, uint32_t pc, const char* name, int indent) {
     bput(g->b, "%*s  %s = iv;\n%*s}\n", indent, "", name, indent, "");
 }
 
-/* One term: its transitions into (best, up), and at t_min its value into cnt (first pass). */
+/* One term: its transitions into best, and at t_min its value into cnt (first pass). */
 static void gen_term(Gen* g, const SPrim* q, int indent) {
     const int first = g->first_pass;
     uint32_t pcs[2] = {q->pcs[0], q->npc > 1u ? q->pcs[1] : 0u};
@@ -686,20 +698,20 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
              "%*s      asm volatile(\"s_mov_b32 %%0, 0x%08x\\n\\ts_mov_b32 %%1, 0x%08x\" : \"=s\"(ka), \"=s\"(kb));\n"
              "%*s      const uint64_t k0 = wodev::event_key_lo(la, ka), k1 = wodev::event_key_lo(lb, kb);\n",
              indent, "", indent, "", indent, "", vl[0], indent, "", vl[1], indent, "", vl[2], indent, "", indent, "",
-             vl[3], indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", o0 << 12,
-             (o0 << 12) | (1u << 11), indent, "");
+             vl[3], indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", term_ka(o0, 1),
+             term_kb(o0, 1), indent, "");
         if (first) bput(g->b, "%*s      cnt += ((la <= tmin) & (lb > tmin)) ? 1u : 0u;\n", indent, "");
         bput(g->b,
              "%*s      WO_WK(WO_WORK_EVENTS);\n"
-             "%*s      wodev::term_cand(k0, (la > tmin)%s, true, best, up);\n"
-             "%*s      wodev::term_cand(k1, (lb > tmin) & (lb < wodev::kInf)%s, false, best, up);\n"
+             "%*s      wodev::term_cand(k0, (la > tmin)%s, best);\n"
+             "%*s      wodev::term_cand(k1, (lb > tmin) & (lb < wodev::kInf)%s, best);\n"
              "%*s    }\n%*s  }\n%*s}\n",
              indent, "", indent, "", after0, indent, "", after1, indent, "", indent, "", indent, "");
         return;
     }
     bput(g->b, "%*s  wodev::Ivl ia;\n", indent, "");
     gen_term_ivl(g, pcs[0], "ia", indent + 2);
-    uint32_t vk[4] = {o0 << 12, (o0 << 12) | (1u << 11), 0u, 0u};
+    uint32_t vk[4] = {term_ka(o0, pos[0]), term_kb(o0, pos[0]), 0u, 0u};
     static const char* nk[4] = {"ka0", "kb0", "ka1", "kb1"};
     if (q->npc == 1u) {
         emit_consts(g->b, indent + 2, "uint32_t", nk, vk, 2);
@@ -707,15 +719,15 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
         if (first) bput(g->b, "%*s  cnt += %swodev::term_in0(x) ? 1u : 0u;\n", indent, "", pos[0] ? "" : "!");
         bput(g->b,
              "%*s  WO_WK(WO_WORK_EVENTS);\n"
-             "%*s  wodev::term_cand(x.kin, x.valid & (x.kin != 0ull)%s, %s, best, up);\n"
-             "%*s  wodev::term_cand(x.kout, x.valid & (x.kout != wodev::kEmptyKey)%s, %s, best, up);\n%*s}\n",
-             indent, "", indent, "", first ? "" : " & (x.kin > after)", pos[0] ? "true" : "false", indent, "",
-             first ? "" : " & (x.kout > after)", pos[0] ? "false" : "true", indent, "");
+             "%*s  wodev::term_cand(x.kin, x.valid & (x.kin != 0ull)%s, best);\n"
+             "%*s  wodev::term_cand(x.kout, x.valid & (x.kout != wodev::kEmptyKey)%s, best);\n%*s}\n",
+             indent, "", indent, "", first ? "" : " & (x.kin > after)", indent, "",
+             first ? "" : " & (x.kout > after)", indent, "");
         return;
     }
     const uint32_t o1 = g->prog[pcs[1]].u1;
-    vk[2] = o1 << 12;
-    vk[3] = (o1 << 12) | (1u << 11);
+    vk[2] = term_ka(o1, pos[1]);
+    vk[3] = term_kb(o1, pos[1]);
     /* a positive first literal empty along every lane's ray: the term is false throughout */
     if (pos[0])
         bput(g->b, "%*s  if (__ballot(!(ia.a > ia.b) & (ia.b > tmin)) != 0ull) {\n", indent, "");
@@ -732,12 +744,11 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
              pos[0] ? "" : "!", pos[1] ? "" : "!");
     bput(g->b,
          "%*s    WO_WK(WO_WORK_EVENTS);\n"
-         "%*s    wodev::term_cands_of<%s, %s, %s>(x, y, after, best, up);\n"
-         "%*s    wodev::term_cands_of<%s, %s, %s>(y, x, after, best, up);\n"
+         "%*s    wodev::term_cands_of<%s, %s>(x, y, after, best);\n"
+         "%*s    wodev::term_cands_of<%s, %s>(y, x, after, best);\n"
          "%*s  }\n%*s}\n",
-         indent, "", indent, "", pos[0] ? "true" : "false", pos[1] ? "true" : "false", first ? "true" : "false",
-         indent, "", pos[1] ? "true" : "false", pos[0] ? "true" : "false", first ? "true" : "false", indent, "",
-         indent, "");
+         indent, "", indent, "", pos[1] ? "true" : "false", first ? "true" : "false", indent, "",
+         pos[0] ? "true" : "false", first ? "true" : "false", indent, "", indent, "");
 }
 
 /* ---- eval, flattened: literal sets as one masked compare ----
@@ -1581,10 +1592,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             bput(&b, "    uint32_t cull[%u];  // bit k: group k culled for this wave\n", ncw);
             for (uint32_t w = 0; w < ncw; ++w) bput(&b, "    cull[%u] = 0u;\n", w);
             bput(&b,
-                 "    // the smallest term transition after `after`, whether it rises, and the\n"
-                 "    // number of terms true at t_min\n"
+                 "    // the smallest term transition after `after` (its rise flag in the key)\n"
+                 "    // and the number of terms true at t_min\n"
                  "    uint64_t best = wodev::kEmptyKey, after = 0ull;\n"
-                 "    bool up = false;\n"
                  "    uint32_t cnt = 0u;\n"
                  "    (void)after;\n"
                  "    WO_MARK(\"collect_begin\");\n"
@@ -1600,8 +1610,11 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  "    for (;;) {\n"
                  "      WO_WK(WO_WORK_SWEEP_STEPS);\n"
                  "      WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);\n"
-                 "      cnt = up ? cnt + 1u : cnt - 1u;\n"
-                 "      if ((cnt != 0u) != root) { wodev::hit_from_key(best, cnt != 0u ? 1u : 0u, hit); return true; }\n"
+                 "      cnt = wodev::term_rises(best) ? cnt + 1u : cnt - 1u;\n"
+                 "      if ((cnt != 0u) != root) {\n"
+                 "        wodev::hit_from_key(wodev::term_event(best), cnt != 0u ? 1u : 0u, hit);\n"
+                 "        return true;\n"
+                 "      }\n"
                  "      // the count moved without flipping the root: the next transition\n"
                  "      after = best;\n"
                  "      best = wodev::kEmptyKey;\n"

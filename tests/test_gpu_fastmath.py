@@ -22,3 +22,4 @@ def test_fast_cr_math_is_exact(which, lo, hi):
     first = ctypes.c_uint32(0)
     assert wl.load().wo_fastmath_check(which, lo, hi, ctypes.byref(bad), ctypes.byref(first)) == 0
     assert bad.value == 0, f"{bad.value} mismatches, first at bits 0x{first.value:08x}"
+

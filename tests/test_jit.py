@@ -586,45 +586,41 @@ static bool sweep(const std::vector<Ivl>& iv, const std::vector<Term>& terms, ui
 // the term method, as the specialised kernel's term mode emits it
 template <bool kFirst>
 static void term_pass(const std::vector<Ivl>& iv, const std::vector<Term>& terms, uint64_t after, uint64_t& best,
-                      bool& up, uint32_t& cnt) {
+                      uint32_t& cnt) {
     for (const Term& t : terms) {
         const uint32_t o0 = t.ord[0];
-        const TermLit x = term_lit(iv[o0], o0 << 12, (o0 << 12) | 2048u);
+        const TermLit x = term_lit(iv[o0], term_ka(o0, t.pos[0]), term_kb(o0, t.pos[0]));
         if (t.n == 1) {
             if (kFirst) cnt += (t.pos[0] ? term_in0(x) : !term_in0(x)) ? 1u : 0u;
-            term_cand(x.kin, x.valid & (x.kin != 0ull) & (kFirst | (x.kin > after)), t.pos[0], best, up);
-            term_cand(x.kout, x.valid & (x.kout != kEmptyKey) & (kFirst | (x.kout > after)), !t.pos[0], best, up);
+            term_cand(x.kin, x.valid & (x.kin != 0ull) & (kFirst | (x.kin > after)), best);
+            term_cand(x.kout, x.valid & (x.kout != kEmptyKey) & (kFirst | (x.kout > after)), best);
             continue;
         }
         if (t.pos[0] && !x.valid) continue;  // the wave-level skip, per lane
         const uint32_t o1 = t.ord[1];
-        const TermLit y = term_lit(iv[o1], o1 << 12, (o1 << 12) | 2048u);
+        const TermLit y = term_lit(iv[o1], term_ka(o1, t.pos[1]), term_kb(o1, t.pos[1]));
         if (kFirst)
             cnt += ((t.pos[0] ? term_in0(x) : !term_in0(x)) & (t.pos[1] ? term_in0(y) : !term_in0(y))) ? 1u : 0u;
-        const int c = (t.pos[0] ? 2 : 0) | (t.pos[1] ? 1 : 0);
-        switch (c) {
-        case 3: term_cands_of<true, true, kFirst>(x, y, after, best, up); term_cands_of<true, true, kFirst>(y, x, after, best, up); break;
-        case 2: term_cands_of<true, false, kFirst>(x, y, after, best, up); term_cands_of<false, true, kFirst>(y, x, after, best, up); break;
-        case 1: term_cands_of<false, true, kFirst>(x, y, after, best, up); term_cands_of<true, false, kFirst>(y, x, after, best, up); break;
-        default: term_cands_of<false, false, kFirst>(x, y, after, best, up); term_cands_of<false, false, kFirst>(y, x, after, best, up); break;
-        }
+        if (t.pos[1]) term_cands_of<true, kFirst>(x, y, after, best);
+        else term_cands_of<false, kFirst>(x, y, after, best);
+        if (t.pos[0]) term_cands_of<true, kFirst>(y, x, after, best);
+        else term_cands_of<false, kFirst>(y, x, after, best);
     }
 }
 
 static bool term_method(const std::vector<Ivl>& iv, const std::vector<Term>& terms, uint64_t& key, bool& after_val) {
     uint64_t best = kEmptyKey;
-    bool up = false;
     uint32_t cnt = 0;
-    term_pass<true>(iv, terms, 0ull, best, up, cnt);
+    term_pass<true>(iv, terms, 0ull, best, cnt);
     if (best == kEmptyKey) return false;
     const bool root = cnt != 0u;
     for (;;) {
-        cnt = up ? cnt + 1u : cnt - 1u;
-        if ((cnt != 0u) != root) { key = best; after_val = cnt != 0u; return true; }
+        cnt = term_rises(best) ? cnt + 1u : cnt - 1u;
+        if ((cnt != 0u) != root) { key = term_event(best); after_val = cnt != 0u; return true; }
         const uint64_t after = best;
         best = kEmptyKey;
         uint32_t unused = 0;
-        term_pass<false>(iv, terms, after, best, up, unused);
+        term_pass<false>(iv, terms, after, best, unused);
         if (best == kEmptyKey) return false;
     }
 }
