@@ -333,7 +333,7 @@ constexpr uint32_t kLaneDepthMax = 24;
 #define WO_LANES_PRIO_LEAF 1  // the same at a sphere leaf's geometry load (single-sphere walks; RTIOW 11.565 -> 11.505 ms)
 #endif
 #ifndef WO_LANES_PRIO_TERM
-#define WO_LANES_PRIO_TERM 0  // the same at a term record's load (term mode; csg512 44.93 -> 44.70 ms in an A/B, not yet verified on by default)
+#define WO_LANES_PRIO_TERM 1  // the same at a term record's load (term mode; csg512 43.44 / 43.39 -> 43.37 / 43.28 ms, parity suite green with it)
 #endif
 #ifndef WO_LANES_FUSED_SPHERE
 #define WO_LANES_FUSED_SPHERE 1
@@ -371,9 +371,11 @@ __device__ __forceinline__ float box_near(float4 lo, float4 hi, F3 ri, F3 oi, fl
 // ray fetch).  Measured and removed: the general BOUND walk,
 // 16-bit stacks for binary trees, 4-wide trees for primitives, resumable binary
 // walks, a uniform grid and fp16 child boxes.
-// events a general-tree walk collects (the smallest after `after`, sorted)
+// events a general-tree walk collects (the smallest after `after`, sorted; with
+// inserts beyond a full window's last filtered out -- csg360_nested 1029 ms at 4,
+// 645 at 8, 503 at 16, 453 at 24, 440 at 32; 48 and 64 spill)
 #ifndef WO_LANES_GWIN
-#define WO_LANES_GWIN 4
+#define WO_LANES_GWIN 32
 #endif
 constexpr int kGWin = WO_LANES_GWIN;
 // a general tree's node record (build_lbvh): left ref | right ref << 15 | op << 30
@@ -641,11 +643,12 @@ struct LaneTracer {
                 // prunes with the largest once it has them all
                 if ((after == 0ull) & (iv.a <= tmin) & (iv.b > tmin)) gtoggle(ord);
                 const uint64_t k0 = event_key(iv.a, ord, 0u, iv.ma), k1 = event_key(iv.b, ord, 1u, iv.mb);
-                if ((iv.a > tmin) & (k0 > after)) {
+                // a key at or beyond a full window's last cannot enter it
+                if ((iv.a > tmin) & (k0 > after) & (k0 < gw[kGWin - 1])) {
                     WO_WK(WO_WORK_EVENTS);
                     ginsert(k0);
                 }
-                if ((iv.b > tmin) & (iv.b < kInf) & (k1 > after)) {
+                if ((iv.b > tmin) & (iv.b < kInf) & (k1 > after) & (k1 < gw[kGWin - 1])) {
                     WO_WK(WO_WORK_EVENTS);
                     ginsert(k1);
                 }
@@ -936,7 +939,9 @@ struct LaneTracer {
             ref = par;
         }
     }
-    __device__ __forceinline__ void ginsert(uint64_t key) {  // the sorted window's insert (Window::insert)
+    // the sorted window's insert (branch-free: an early exit once no lane shifts
+    // measured slower, 488 against 440 ms on csg360_nested)
+    __device__ __forceinline__ void ginsert(uint64_t key) {
 #pragma unroll
         for (int i = kGWin - 1; i > 0; --i) gw[i] = key < gw[i - 1] ? gw[i - 1] : (key < gw[i] ? key : gw[i]);
         gw[0] = key < gw[0] ? key : gw[0];
