@@ -44,7 +44,7 @@ def main():
            "-Rpass-analysis=kernel-resource-usage"] + [f"-D{x}" for x in a.D]
     res = subprocess.run(cmd, capture_output=True, text=True)
     for line in res.stderr.splitlines():
-        m = re.search(r"remark:\s+(VGPRs|TotalSGPRs|ScratchSize.*|Occupancy.*|SGPRs Spill|VGPRs Spill):\s*(\d+)", line)
+        m = re.search(r"remark:\s+(VGPRs|TotalSGPRs|ScratchSize.*|Occupancy.*|SGPRs Spill|VGPRs Spill|LDS Size.*):\s*(\d+)", line)
         if m:
             print(f"{m.group(1)}: {m.group(2)}")
     if res.returncode:
