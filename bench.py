@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--tile-rows", type=int, default=4)
+    ap.add_argument("--band", default="auto",
+                    help="row-band weighting of an N-rank frame, CYCLE:SKIP: rank 0, which also receives the "
+                         "gather and assembles, sits out SKIP of every CYCLE rounds of bands; 'auto' = "
+                         "wololo.default_band(N), '0:0' = one band per rank and round")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count-work", action="store_true",
@@ -172,7 +176,10 @@ def main():
     params = info.params(**over)
     r.set_tracer("interpreter" if args.jit == 0 else args.tracer)
     W, H, T = params.width, params.height, args.tile_rows
-    lr = wl.local_rows(H, T, world)
+    band = wl.default_band(world) if args.band == "auto" else tuple(int(x) for x in args.band.split(":"))
+    args.band_w = band if world > 1 else (0, 0)
+    r.set_band_weight(*args.band_w)
+    lr = wl.local_rows(H, T, world, args.band_w)
     # the same two-buffer / two-stream / event code runs on either backend, so a gloo
     # rehearsal on one GPU executes what the RCCL run on 8 GPUs does
     pipelined = world > 1 and not args.no_pipeline
@@ -221,7 +228,7 @@ def main():
             if rank == 0:
                 dist.gather(src, gather_list=gathered, dst=0)
                 g = stacked.to(dev, non_blocking=False) if gloo else stacked
-                wl.assemble_rows_device(g.data_ptr(), frame.data_ptr(), W, H, T, world, cs.cuda_stream)
+                wl.assemble_rows_device(g.data_ptr(), frame.data_ptr(), W, H, T, world, cs.cuda_stream, args.band_w)
             else:
                 dist.gather(src, dst=0)
             if pipelined:
@@ -307,7 +314,8 @@ def main():
         line = report_line(args, r, info, params, world, elapsed_s, segs_all, segs_local, k_ms, work,
                            {"parallelism": parallelism, "ranks": world, "devices": min(world, ndev),
                             "launcher": "torchrun" if world_env else "none",
-                            "frames_in_flight": args.frames_in_flight, "prewarm_frames": prewarm})
+                            "frames_in_flight": args.frames_in_flight, "prewarm_frames": prewarm,
+                            **({"row_bands": f"{args.band_w[0]}:{args.band_w[1]}"} if world > 1 else {})})
         if verified is not None:
             line["verified_vs_full_render"] = verified
         if world == 1 and info.mode == wl.MODE_PATHTRACE and not args.no_draw_frame:
@@ -420,7 +428,8 @@ def report_line(args, r, info, params, world, elapsed_s, segs_all, segs_local, k
     segments one launch traced (segs_local over the steps)."""
     from csgrenderer_amd import wololo as wl
     W, H, T = params.width, params.height, args.tile_rows
-    lr = wl.local_rows(H, T, world)
+    band = getattr(args, "band_w", (0, 0))
+    lr = min(wl.rank_bands(H, T, 0, world, band) * T, wl.local_rows(H, T, world, band))  # rank 0's rows
     steps = args.steps
     ms_per_step = elapsed_s / steps * 1e3
     samples = W * H * (params.spp if info.mode == wl.MODE_PATHTRACE else 1)

@@ -472,6 +472,10 @@ int wo_renderer_frame_desc(Wo_Renderer* r, Wo_RenderParams const* p, uint32_t ti
     out->tile_rows = tile_rows;
     out->rank = rank;
     out->nranks = nranks;
+    if (nranks > 1u) {
+        out->band_cycle = r->band_cycle;
+        out->band_skip = r->band_skip;
+    }
     out->n_recs = r->n_recs;
     out->n_prims = r->n_prims;
     out->time_sec = p->time_sec;
@@ -695,13 +699,31 @@ int wo_renderer_count_work(Wo_Renderer* r, Wo_RenderParams const* params, uint32
     return 0;
 }
 
-int wo_assemble_rows_device(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,
-                            uint32_t tile_rows, uint32_t nranks, void* stream) {
+int wo_assemble_rows_device_ex(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,
+                               uint32_t tile_rows, uint32_t nranks, uint32_t band_cycle, uint32_t band_skip,
+                               void* stream) {
     char err[256] = {0};
-    if (wo_dev_assemble(d_gathered, d_frame, width, height, tile_rows, nranks, stream, err, sizeof err)) {
+    if (wo_dev_assemble(d_gathered, d_frame, width, height, tile_rows, nranks, band_cycle, band_skip, stream, err,
+                        sizeof err)) {
         wo_set_error("%s", err);
         return -1;
     }
+    return 0;
+}
+
+int wo_assemble_rows_device(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,
+                            uint32_t tile_rows, uint32_t nranks, void* stream) {
+    return wo_assemble_rows_device_ex(d_gathered, d_frame, width, height, tile_rows, nranks, 0u, 0u, stream);
+}
+
+int wo_renderer_set_band_weight(Wo_Renderer* r, uint32_t band_cycle, uint32_t band_skip) {
+    if (!r) return -1;
+    if (band_skip != 0u && band_skip >= band_cycle) {
+        wo_set_error("band weight: skip %u must be below the cycle %u (or 0)", band_skip, band_cycle);
+        return -1;
+    }
+    r->band_cycle = band_skip ? band_cycle : 0u;
+    r->band_skip = band_skip;
     return 0;
 }
 

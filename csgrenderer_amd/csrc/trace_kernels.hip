@@ -1207,13 +1207,14 @@ __global__ __launch_bounds__(kBlock) void work_collect_kernel(unsigned long long
 
 __global__ __launch_bounds__(kBlock) void assemble_kernel(const float4* __restrict__ gathered, float4* __restrict__ frame,
                                                           uint32_t W, uint32_t H, uint32_t T, uint32_t N,
-                                                          uint32_t local_rows) {
+                                                          uint32_t cycle, uint32_t skip, uint32_t local_rows) {
     size_t total = (size_t)W * H;
     for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += (size_t)gridDim.x * kBlock) {
         uint32_t y = (uint32_t)(i / W), x = (uint32_t)(i - (size_t)y * W);
         uint32_t g = y / T;
-        uint32_t r = g % N;
-        uint32_t lrow = (g / N) * T + (y - g * T);
+        uint32_t r, lb;
+        band_local(g, N, cycle, skip, r, lb);
+        uint32_t lrow = lb * T + (y - g * T);
         frame[i] = gathered[((size_t)r * local_rows + lrow) * W + x];
     }
 }
@@ -2580,11 +2581,11 @@ extern "C" double wo_dev_jit_compile_sec(WoDev* dev) { return dev ? dev->jit_com
 // while the frame holds >= 8 rounds of such tiles, else 8x4 (2-round tail), else 4x4
 // (plan_tiles); `resident` = workgroups the device holds at once.  Env (measurements):
 // WOLOLO_TILE=8x8|8x4|4x4 forces one shape everywhere, with no tail.
-// "WxH" with W, H in {1, 2, 4, 8} and W*H <= kTileMaxPix; 0 if not such a shape
+// "WxH" with W, H in {1, 2, 4, 8, 16} and W*H <= kTileMaxPix; 0 if not such a shape
 static uint32_t shape_of(const char* f) {
     unsigned w = 0, h = 0;
     if (sscanf(f, "%ux%u", &w, &h) != 2) return 0u;
-    auto lg = [](unsigned v) -> int { return v == 1u ? 0 : v == 2u ? 1 : v == 4u ? 2 : v == 8u ? 3 : -1; };
+    auto lg = [](unsigned v) -> int { return v == 1u ? 0 : v == 2u ? 1 : v == 4u ? 2 : v == 8u ? 3 : v == 16u ? 4 : -1; };
     const int lw = lg(w), lh = lg(h);
     if (lw < 0 || lh < 0 || w * h > kTileMaxPix) return 0u;
     return (uint32_t)lw | ((uint32_t)lh << 4);
@@ -2613,7 +2614,10 @@ static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, u
         // 1080p64, slowest rank of 4 / 8, ms): csg32 8x8 1.454 / 0.770, 8x4 1.400 /
         // 0.762, 4x4 1.499 / 0.786; csg256 balanced 8x4 4.73 / 3.50, 4x4 4.23 / 2.34;
         // csg256 chain 8x4 7.34 / 5.02, 4x4 7.99 / 4.15; rtiow 8x4 8.47 / 4.30,
-        // 4x4 8.27 / 4.37.  One GPU keeps 8x8 (csg32 5.18 vs 5.37 ms at 8x4).
+        // 4x4 8.27 / 4.37.  One GPU keeps 8x8 (csg32 5.18 vs 5.37 ms at 8x4).  Round 4
+        // (tools/root_step.py, N = 8 projection): 3 tiles per resident workgroup instead
+        // of 8 (8x4 at N = 8): csg32 6.37 -> 6.62x, csg256 balanced 6.79 -> 4.18x,
+        // chain 6.83 -> 4.75x, csg32_nested 6.35 -> 5.83x, RTIOW 6.59 -> 6.63x; kept at 8.
         const uint64_t want_tiles = 8ull * resident;
         big = 3u | (3u << 4);
         if ((uint64_t)tiles_across(width, big) * (rows >> 3) < want_tiles || band_rows < 8u) {
@@ -2738,7 +2742,7 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
         set_err(err, errlen, "hipSetDevice", e);
         return -1;
     }
-    uint32_t local_rows = wo_rank_local_rows(fr.height, fr.tile_rows, fr.nranks);
+    uint32_t local_rows = wo_rank_local_rows_ex(fr.height, fr.tile_rows, fr.nranks, fr.band_cycle, fr.band_skip);
     float4* out = (float4*)d_out;
 
     if (fr.mode == WO_MODE_UBERSHADER_RT1 || fr.mode == WO_MODE_DEBUG_ST) {
@@ -2882,7 +2886,7 @@ extern "C" int wo_dev_count_work(WoDev* dev, WoFrame const* frame, unsigned long
         if (jit_code(dev->jit_src.c_str(), dev->arch, true, code, key, origin, sec, err, errlen)) return -1;
         if (load_jit_module(code, &dev->count_module, &dev->count_fn, err, errlen)) return -1;
     }
-    const size_t local_rows = wo_rank_local_rows(fr.height, fr.tile_rows, fr.nranks);
+    const size_t local_rows = wo_rank_local_rows_ex(fr.height, fr.tile_rows, fr.nranks, fr.band_cycle, fr.band_skip);
     if (ensure_buffer(&dev->d_frame, &dev->frame_cap, local_rows * fr.width * sizeof(float4), err, errlen)) return -1;
     if (!dev->d_work) {
         e = hipMalloc((void**)&dev->d_work, WO_WORK_KINDS * sizeof(unsigned long long));
@@ -3203,6 +3207,7 @@ static int ranks_render_assemble(WoDev* const* devs, uint32_t n, WoFrame fr, int
     WoDev* root = devs[0];
     fr.tile_rows = 4;
     fr.nranks = n;
+    fr.band_cycle = fr.band_skip = 0u;  // the C API's device ranks: one band per rank and round
     const uint32_t lr = wo_rank_local_rows(fr.height, fr.tile_rows, n);
     const size_t share = (size_t)lr * fr.width;  // float4s per rank
     hipError_t e = hipSetDevice(root->device);
@@ -3299,7 +3304,8 @@ static int ranks_render_assemble(WoDev* const* devs, uint32_t n, WoFrame fr, int
             return -1;
         }
     }
-    if (wo_dev_assemble(root->d_gather[slot], dst, fr.width, fr.height, fr.tile_rows, n, s_out, err, errlen)) return -1;
+    if (wo_dev_assemble(root->d_gather[slot], dst, fr.width, fr.height, fr.tile_rows, n, 0u, 0u, s_out, err, errlen))
+        return -1;
     // the slot's buffers are free once the assembly has read them
     e = hipEventRecord(root->gate_ev[slot], s_out);
     if (e != hipSuccess) {
@@ -3444,18 +3450,20 @@ extern "C" int wo_dev_srgb8(void const* d_rgba, void* d_bgra8, size_t pixels, vo
 }
 
 extern "C" int wo_dev_assemble(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,
-                               uint32_t tile_rows, uint32_t nranks, void* stream, char* err, size_t errlen) {
+                               uint32_t tile_rows, uint32_t nranks, uint32_t cycle, uint32_t skip, void* stream,
+                               char* err, size_t errlen) {
     if (tile_rows == 0 || nranks == 0) {
         snprintf(err, errlen, "bad tiling");
         return -1;
     }
-    uint32_t local_rows = wo_rank_local_rows(height, tile_rows, nranks);
+    uint32_t local_rows = wo_rank_local_rows_ex(height, tile_rows, nranks, cycle, skip);
     size_t total = (size_t)width * height;
     uint32_t blocks = (uint32_t)((total + kBlock - 1) / kBlock);
     if (blocks > 8192u) blocks = 8192u;
     if (blocks == 0) return 0;
     hipLaunchKernelGGL(assemble_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream,
-                       (const float4*)d_gathered, (float4*)d_frame, width, height, tile_rows, nranks, local_rows);
+                       (const float4*)d_gathered, (float4*)d_frame, width, height, tile_rows, nranks, cycle, skip,
+                       local_rows);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_err(err, errlen, "assemble launch", e);

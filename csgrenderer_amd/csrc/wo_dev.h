@@ -163,7 +163,8 @@ int wo_dev_count_work(WoDev* dev, WoFrame const* frame, unsigned long long* coun
 int wo_dev_render_host(WoDev* dev, WoFrame const* frame, float* host_rgba, char* err, size_t errlen);
 /* Un-interleave gathered rank buffers into a frame (async on `stream`). */
 int wo_dev_assemble(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,
-                    uint32_t tile_rows, uint32_t nranks, void* stream, char* err, size_t errlen);
+                    uint32_t tile_rows, uint32_t nranks, uint32_t band_cycle, uint32_t band_skip, void* stream,
+                    char* err, size_t errlen);
 
 #ifdef __cplusplus
 }

@@ -102,6 +102,7 @@ struct Wo_Renderer {
     uint32_t last_w, last_h;
     int last_slot;               /* the presented frame's slot (-1: none) */
     int map_float;               /* copy every presented float frame to the host (else on demand) */
+    uint32_t band_cycle, band_skip; /* weighted row bands of a multi-rank frame (wo_renderer_set_band_weight) */
     /* pipeline timestamps (wo_renderer_set_frame_stamps): per presented frame,
      * render begin / render end / map-back end in ms */
     int stamps;

@@ -69,7 +69,8 @@ class WoCamera(Structure):
 class WoFrame(Structure):
     _fields_ = [("width", c_uint32), ("height", c_uint32), ("spp", c_uint32), ("max_depth", c_uint32),
                 ("seed", c_uint32), ("mode", c_uint32), ("sample_offset", c_uint32), ("tile_rows", c_uint32),
-                ("rank", c_uint32), ("nranks", c_uint32), ("n_recs", c_uint32), ("n_prims", c_uint32),
+                ("rank", c_uint32), ("nranks", c_uint32), ("band_cycle", c_uint32), ("band_skip", c_uint32),
+                ("n_recs", c_uint32), ("n_prims", c_uint32),
                 ("time_sec", c_float), ("sphere_y", c_float), ("inv_width", c_float), ("inv_height", c_float),
                 ("cam", WoCamera)]
 
@@ -113,6 +114,9 @@ SIGNATURES = {
     "wo_renderer_count_work": (c_int, [c_void_p, POINTER(RenderParams), c_uint32, c_uint32, c_uint32,
                                        POINTER(c_ulonglong)]),
     "wo_assemble_rows_device": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_void_p]),
+    "wo_assemble_rows_device_ex": (c_int, [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32,
+                                           c_uint32, c_void_p]),
+    "wo_renderer_set_band_weight": (c_int, [c_void_p, c_uint32, c_uint32]),
     "wo_renderer_set_devices": (c_int, [c_void_p, c_int]),
     "wo_renderer_device_count": (c_int, [c_void_p]),
     "wo_renderer_frame_ranks": (c_int, [c_void_p, POINTER(RenderParams)]),
@@ -451,6 +455,11 @@ class Renderer:
             raise WololoError(last_error())
         return dict(zip(WORK_KINDS, (int(v) for v in c)))
 
+    def set_band_weight(self, cycle: int, skip: int):
+        """Weighted row bands of multi-rank frames: rank 0 sits out `skip` of every `cycle` rounds."""
+        if self.lib.wo_renderer_set_band_weight(self.ptr, cycle, skip):
+            raise WololoError(last_error())
+
     def render_rows_device(self, params: RenderParams, d_out: int, tile_rows: int, rank: int, nranks: int,
                            stream: int = 0, d_segments: int = 0):
         if self.lib.wo_renderer_render_rows_device(self.ptr, ctypes.byref(params), c_void_p(d_out), tile_rows, rank,
@@ -465,10 +474,11 @@ def render_params(width=256, height=256, spp=1, max_depth=8, seed=0, mode=MODE_U
 
 
 def assemble_rows_device(d_gathered: int, d_frame: int, width: int, height: int, tile_rows: int, nranks: int,
-                         stream: int = 0):
+                         stream: int = 0, band=(0, 0)):
+    """Un-interleave the gathered rank buffers; `band` = (cycle, skip) of weighted bands."""
     lib = load()
-    if lib.wo_assemble_rows_device(c_void_p(d_gathered), c_void_p(d_frame), width, height, tile_rows, nranks,
-                                   c_void_p(stream or None)):
+    if lib.wo_assemble_rows_device_ex(c_void_p(d_gathered), c_void_p(d_frame), width, height, tile_rows, nranks,
+                                      band[0], band[1], c_void_p(stream or None)):
         raise WololoError(last_error())
 
 
@@ -523,12 +533,54 @@ def jit_compile_check(src: str, arch: str = "gfx950") -> str:
     return "" if rc == 0 else err.value.decode(errors="replace")
 
 
-def local_rows(height: int, tile_rows: int, nranks: int) -> int:
-    """Mirror of wo_rank_local_rows() (wo_scene.h)."""
+def _weighted(nranks, band):
+    return nranks >= 2 and 0 < band[1] < band[0]
+
+
+def band_global(lb: int, rank: int, nranks: int, band=(0, 0)) -> int:
+    """Mirror of wo_band_global() (wo_scene.h): the frame band of a rank's local band."""
+    if not _weighted(nranks, band):
+        return lb * nranks + rank
+    cycle, skip = band
+    full = cycle - skip
+    per = full if rank == 0 else cycle
+    c, j = divmod(lb, per)
+    p = j * nranks + rank if j < full else full * nranks + (j - full) * (nranks - 1) + rank - 1
+    return c * (cycle * nranks - skip) + p
+
+
+def rank_bands(height: int, tile_rows: int, rank: int, nranks: int, band=(0, 0)) -> int:
+    """Mirror of wo_rank_tile_count_ex() (wo_scene.h)."""
     tiles = (height + tile_rows - 1) // tile_rows
-    return ((tiles + nranks - 1) // nranks) * tile_rows
+    if not _weighted(nranks, band):
+        return (tiles - rank + nranks - 1) // nranks if rank < tiles else 0
+    cycle, skip = band
+    per = cycle - skip if rank == 0 else cycle
+    c, rem = divmod(tiles, cycle * nranks - skip)
+    return c * per + sum(1 for j in range(per) if band_global(j, rank, nranks, band) < rem)
 
 
-def global_row(lrow: int, tile_rows: int, rank: int, nranks: int) -> int:
+def default_band(nranks: int):
+    """The row-band weighting bench.py gives an N-rank frame: rank 0 (which also
+    receives the gather, assembles and presents) sits out one round of bands in
+    every `cycle`.  tools/root_step.py, csg32 1080p64, N = 8: 0:0 6.21x, 8:1 6.37x,
+    12:1 6.44x; N = 4: 0:0 3.33x, 16:1 3.59x; N = 2: 0:0 1.89x, 32:1 1.92x.  Heavier
+    scenes want a lighter skip (rank 0's extra work is the same milliseconds)."""
+    if nranks >= 8:
+        return (10, 1)
+    if nranks >= 4:
+        return (16, 1)
+    if nranks >= 2:
+        return (32, 1)
+    return (0, 0)
+
+
+def local_rows(height: int, tile_rows: int, nranks: int, band=(0, 0)) -> int:
+    """Mirror of wo_rank_local_rows_ex() (wo_scene.h)."""
+    t = [rank_bands(height, tile_rows, r, nranks, band) for r in range(min(nranks, 2))]
+    return max(t) * tile_rows
+
+
+def global_row(lrow: int, tile_rows: int, rank: int, nranks: int, band=(0, 0)) -> int:
     lt = lrow // tile_rows
-    return (lt * nranks + rank) * tile_rows + (lrow - lt * tile_rows)
+    return band_global(lt, rank, nranks, band) * tile_rows + (lrow - lt * tile_rows)

@@ -87,6 +87,17 @@ int wo_renderer_count_work(Wo_Renderer* r, Wo_RenderParams const* params, uint32
  * wo_rank_local_rows(...) * width float4s) into a width*height float4 frame. */
 int wo_assemble_rows_device(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,
                             uint32_t tile_rows, uint32_t nranks, void* stream);
+/* The same for row bands weighted by wo_renderer_set_band_weight (buffers of
+ * wo_rank_local_rows_ex(..., band_cycle, band_skip) rows). */
+int wo_assemble_rows_device_ex(void const* d_gathered, void* d_frame, uint32_t width, uint32_t height,
+                               uint32_t tile_rows, uint32_t nranks, uint32_t band_cycle, uint32_t band_skip,
+                               void* stream);
+/* Row bands of the renderer's multi-rank frames (render_rows_device, count_work
+ * with nranks > 1): in every band_cycle rounds of the ranks rank 0 sits out
+ * band_skip (0 = a band per rank and round, the default), so the rank that also
+ * gathers, assembles and presents renders less (wo_scene.h wo_band_global).
+ * -1 if 0 < band_skip >= band_cycle. */
+int wo_renderer_set_band_weight(Wo_Renderer* r, uint32_t band_cycle, uint32_t band_skip);
 
 /* ---- several GPUs per renderer ----
  * The reference renders on physical device 0 only (renderer.c:519-520).  Here

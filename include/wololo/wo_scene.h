@@ -106,7 +106,9 @@ typedef struct WoFrame {
     uint32_t mode;              /* WO_MODE_* */
     uint32_t sample_offset;     /* first sample index */
     uint32_t tile_rows;         /* row-cyclic tiling: tile height in rows */
-    uint32_t rank, nranks;      /* this device renders tiles g with g % nranks == rank */
+    uint32_t rank, nranks;      /* this device renders row bands (tiles) of the frame: wo_band_global */
+    uint32_t band_cycle;        /* band weighting: in every band_cycle rounds of the ranks, rank 0 */
+    uint32_t band_skip;         /* sits out band_skip rounds (0: every rank takes one band per round) */
     uint32_t n_recs;            /* program length */
     uint32_t n_prims;           /* primitive count */
     float time_sec;             /* ubershader: UBO time_since_start_sec */
@@ -143,16 +145,68 @@ enum {
 /* Minimum ray parameter for every CSG segment (RTIOW's 0.001). */
 #define WO_T_MIN (1.0e-3f)
 
-/* Number of tile rows a rank owns for a frame of `height` rows. */
+/* Row bands of tile_rows frame rows go to the ranks in rounds: band g of a plain
+ * partition (skip = 0) is rank g % n's local band g / n.  With weighting (0 < skip
+ * < cycle, n >= 2), every cycle of `cycle` rounds holds cycle * n - skip bands:
+ * rounds [0, cycle - skip) give one band to every rank in rank order, the last
+ * `skip` rounds one to every rank but 0 -- rank 0, which also gathers, assembles
+ * and presents the frame, renders (cycle - skip) / cycle of another rank's share.
+ * (Mirrored by wo_device_common.h local_to_global_row and wololo.py global_row.) */
+static inline int wo_band_weighted(uint32_t n, uint32_t cycle, uint32_t skip) {
+    return n >= 2u && skip > 0u && skip < cycle;
+}
+/* the frame band of rank `rank`'s local band lb */
+static inline uint32_t wo_band_global(uint32_t lb, uint32_t rank, uint32_t n, uint32_t cycle, uint32_t skip) {
+    if (!wo_band_weighted(n, cycle, skip)) return lb * n + rank;
+    const uint32_t full = cycle - skip, per = rank == 0u ? full : cycle;
+    const uint32_t c = lb / per, j = lb - c * per;
+    const uint32_t p = j < full ? j * n + rank : full * n + (j - full) * (n - 1u) + rank - 1u;
+    return c * (cycle * n - skip) + p;
+}
+/* the rank and local band of frame band g */
+static inline void wo_band_local(uint32_t g, uint32_t n, uint32_t cycle, uint32_t skip, uint32_t* rank,
+                                 uint32_t* lb) {
+    if (!wo_band_weighted(n, cycle, skip)) {
+        *rank = g % n;
+        *lb = g / n;
+        return;
+    }
+    const uint32_t full = cycle - skip, len = cycle * n - skip, c = g / len, p = g - c * len;
+    if (p < full * n) {
+        const uint32_t j = p / n, r = p - j * n;
+        *rank = r;
+        *lb = c * (r == 0u ? full : cycle) + j;
+    } else {
+        const uint32_t q = p - full * n, j = full + q / (n - 1u), r = 1u + q % (n - 1u);
+        *rank = r;
+        *lb = c * cycle + j;
+    }
+}
+/* Number of bands (tile rows) a rank owns for a frame of `height` rows. */
+static inline uint32_t wo_rank_tile_count_ex(uint32_t height, uint32_t tile_rows, uint32_t rank, uint32_t nranks,
+                                             uint32_t cycle, uint32_t skip) {
+    const uint32_t tiles = (height + tile_rows - 1u) / tile_rows;
+    if (!wo_band_weighted(nranks, cycle, skip)) return rank < tiles ? (tiles - rank + nranks - 1u) / nranks : 0u;
+    const uint32_t full = cycle - skip, per = rank == 0u ? full : cycle, len = cycle * nranks - skip;
+    const uint32_t c = tiles / len, rem = tiles - c * len;
+    uint32_t cnt = c * per;
+    for (uint32_t j = 0; j < per; ++j) cnt += wo_band_global(j, rank, nranks, cycle, skip) < rem ? 1u : 0u;
+    return cnt;
+}
 static inline uint32_t wo_rank_tile_count(uint32_t height, uint32_t tile_rows, uint32_t rank, uint32_t nranks) {
-    uint32_t tiles = (height + tile_rows - 1u) / tile_rows;
-    return rank < tiles ? (tiles - rank + nranks - 1u) / nranks : 0u;
+    return wo_rank_tile_count_ex(height, tile_rows, rank, nranks, 0u, 0u);
 }
 
-/* Rows in one rank's local (gather) buffer: the same for every rank. */
+/* Rows in one rank's local (gather) buffer: the same for every rank, the most any
+ * rank owns (rank 0 or 1: a rank owns no more bands than a lower one but 0). */
+static inline uint32_t wo_rank_local_rows_ex(uint32_t height, uint32_t tile_rows, uint32_t nranks, uint32_t cycle,
+                                             uint32_t skip) {
+    const uint32_t t0 = wo_rank_tile_count_ex(height, tile_rows, 0u, nranks, cycle, skip);
+    const uint32_t t1 = nranks > 1u ? wo_rank_tile_count_ex(height, tile_rows, 1u, nranks, cycle, skip) : 0u;
+    return (t0 > t1 ? t0 : t1) * tile_rows;
+}
 static inline uint32_t wo_rank_local_rows(uint32_t height, uint32_t tile_rows, uint32_t nranks) {
-    uint32_t tiles = (height + tile_rows - 1u) / tile_rows;
-    return ((tiles + nranks - 1u) / nranks) * tile_rows;
+    return wo_rank_local_rows_ex(height, tile_rows, nranks, 0u, 0u);
 }
 
 #ifdef __cplusplus

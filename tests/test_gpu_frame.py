@@ -226,6 +226,14 @@ def test_host_staged_gather_equals_one_device(monkeypatch):
     _cmp(g1, acc1, "accumulation 1, host-staged")
     _cmp(g2, acc2, "accumulation 2, host-staged")
     _cmp(_device_frame(r, p), one, "device frame, host-staged gather")
+    # a staged device frame still queued when the ranks are retired (its H2D copies read
+    # the ranks' pinned buffers on the root's stream): set_devices waits for the root
+    import torch
+    f = torch.full((p.height, p.width, 4), -1.0, dtype=torch.float32, device="cuda")
+    r.render_frame_device(p, f.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert r.set_devices(1) == 1
+    torch.cuda.synchronize()
+    _cmp(f.cpu().numpy(), one, "device frame queued before set_devices(1)")
     r.close()
 
 

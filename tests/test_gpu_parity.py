@@ -235,20 +235,24 @@ def _torch():
 
 
 @pytest.mark.parametrize("path", PATHS)
-@pytest.mark.parametrize("nranks,tile", [(1, 16), (2, 16), (3, 8), (8, 16), (5, 7)])
-def test_row_tiles_assemble_to_full_frame(nranks, tile, path):
+@pytest.mark.parametrize("nranks,tile,band", [(1, 16, (0, 0)), (2, 16, (0, 0)), (3, 8, (0, 0)), (8, 16, (0, 0)),
+                                              (5, 7, (0, 0)), (3, 8, (2, 1)), (8, 4, (8, 1)), (4, 4, (3, 2))])
+def test_row_tiles_assemble_to_full_frame(nranks, tile, band, path):
+    """`band`: weighted row bands (wo_renderer_set_band_weight: rank 0 sits out `skip`
+    of every `cycle` rounds), as bench.py gives N-rank frames."""
     torch = _torch()
     r, info = _scene("csg32", path)
     p = info.params(width=200, height=123, spp=2)
     full = r.render(p)
-    lr = wl.local_rows(p.height, tile, nranks)
+    r.set_band_weight(*band)
+    lr = wl.local_rows(p.height, tile, nranks, band)
     gathered = torch.zeros((nranks, lr, p.width, 4), dtype=torch.float32, device="cuda")
     seg = torch.zeros(1, dtype=torch.int64, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     for rank in range(nranks):
         r.render_rows_device(p, gathered[rank].data_ptr(), tile, rank, nranks, stream, seg.data_ptr())
     frame = torch.empty((p.height, p.width, 4), dtype=torch.float32, device="cuda")
-    wl.assemble_rows_device(gathered.data_ptr(), frame.data_ptr(), p.width, p.height, tile, nranks, stream)
+    wl.assemble_rows_device(gathered.data_ptr(), frame.data_ptr(), p.width, p.height, tile, nranks, stream, band)
     torch.cuda.synchronize()
     assert np.array_equal(frame.cpu().numpy(), full)
     # segment counter == oracle's count for the whole frame

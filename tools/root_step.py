@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--no-encode", action="store_true")
     ap.add_argument("--tile-rows", type=int, default=4, help="rows per row-cyclic band (bench.py --tile-rows)")
+    ap.add_argument("--band", default="auto",
+                    help="row-band weighting CYCLE:SKIP (rank 0 sits out SKIP of every CYCLE rounds), 'auto' = "
+                         "wololo.default_band(N) as bench.py uses it, '0:0' = a band per rank and round")
     ap.add_argument("--map-back", default="bgra", choices=["bgra", "float", "none"],
                     help="rank 0's D2H of the presented frame after the encode (draw_frame: bgra)")
     args = ap.parse_args()
@@ -95,7 +98,9 @@ def main():
     hf = [torch.empty((H, W, 4), dtype=torch.float32).pin_memory() for _ in range(2)] \
         if mapback and args.map_back == "float" else []
     for n in args.worlds:
-        lr = wl.local_rows(H, T, n)
+        band = wl.default_band(n) if args.band == "auto" else tuple(int(x) for x in args.band.split(":"))
+        r.set_band_weight(*band)
+        lr = wl.local_rows(H, T, n, band)
         share_bytes = lr * W * 16
         rs = [torch.cuda.Stream(), torch.cuda.Stream()]
         cps, asm, d2h = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
@@ -135,7 +140,8 @@ def main():
                 asm.wait_event(copied)
                 if mapped[b] is not None:
                     asm.wait_event(mapped[b])
-                wl.assemble_rows_device(gather[b].data_ptr(), frames[b].data_ptr(), W, H, T, n, asm.cuda_stream)
+                wl.assemble_rows_device(gather[b].data_ptr(), frames[b].data_ptr(), W, H, T, n, asm.cuda_stream,
+                                        band)
                 if not args.no_encode:
                     wl.srgb8_encode_device(frames[b].data_ptr(), bgra[b].data_ptr(), W * H, asm.cuda_stream)
                 ev = torch.cuda.Event()
@@ -159,10 +165,11 @@ def main():
         others = [timed(share(k)) for k in range(1, n)]
         worst_other = max(others) if others else 0.0
         proj = max(root_ms, worst_other)
-        res["worlds"][n] = {"root_step_ms": round(root_ms, 4), "other_share_ms": [round(x, 4) for x in others],
+        res["worlds"][n] = {"band": list(band), "root_step_ms": round(root_ms, 4),
+                            "other_share_ms": [round(x, 4) for x in others],
                             "share_bytes": share_bytes, "projected_frame_ms": round(proj, 4),
                             "projected_speedup": round(t1 / proj, 3)}
-        print(f"[root] N={n} rank 0 step {root_ms:.3f} ms (share + {n - 1} copies of {share_bytes / 1e6:.1f} MB "
+        print(f"[root] N={n} band {band[0]}:{band[1]} rank 0 step {root_ms:.3f} ms (share + {n - 1} copies of {share_bytes / 1e6:.1f} MB "
               f"+ assemble{'' if args.no_encode else ' + encode'}{' + D2H ' + args.map_back if mapback else ''}), "
               f"slowest other share {worst_other:.3f} ms "
               f"-> {proj:.3f} ms per frame, {t1 / proj:.2f}x", flush=True)
