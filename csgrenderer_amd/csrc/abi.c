@@ -35,9 +35,8 @@ static const AbiField kAbi[] = {
     F(WoCamera, u), F(WoCamera, v), F(WoCamera, lens_radius), F(WoCamera, pad),
     T(WoFrame), F(WoFrame, width), F(WoFrame, height), F(WoFrame, spp), F(WoFrame, max_depth), F(WoFrame, seed),
     F(WoFrame, mode), F(WoFrame, sample_offset), F(WoFrame, tile_rows), F(WoFrame, rank), F(WoFrame, nranks),
-    F(WoFrame, band_cycle), F(WoFrame, band_skip),
     F(WoFrame, n_recs), F(WoFrame, n_prims), F(WoFrame, time_sec), F(WoFrame, sphere_y), F(WoFrame, inv_width),
-    F(WoFrame, inv_height), F(WoFrame, cam),
+    F(WoFrame, inv_height), F(WoFrame, cam), F(WoFrame, band_cycle), F(WoFrame, band_skip),
 };
 
 #undef T

@@ -69,10 +69,9 @@ class WoCamera(Structure):
 class WoFrame(Structure):
     _fields_ = [("width", c_uint32), ("height", c_uint32), ("spp", c_uint32), ("max_depth", c_uint32),
                 ("seed", c_uint32), ("mode", c_uint32), ("sample_offset", c_uint32), ("tile_rows", c_uint32),
-                ("rank", c_uint32), ("nranks", c_uint32), ("band_cycle", c_uint32), ("band_skip", c_uint32),
-                ("n_recs", c_uint32), ("n_prims", c_uint32),
+                ("rank", c_uint32), ("nranks", c_uint32), ("n_recs", c_uint32), ("n_prims", c_uint32),
                 ("time_sec", c_float), ("sphere_y", c_float), ("inv_width", c_float), ("inv_height", c_float),
-                ("cam", WoCamera)]
+                ("cam", WoCamera), ("band_cycle", c_uint32), ("band_skip", c_uint32)]
 
 
 assert ctypes.sizeof(Vec3) == 24 and ctypes.sizeof(Quaternion) == 32 and ctypes.sizeof(NodeArgument) == 64

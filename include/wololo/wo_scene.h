@@ -107,14 +107,14 @@ typedef struct WoFrame {
     uint32_t sample_offset;     /* first sample index */
     uint32_t tile_rows;         /* row-cyclic tiling: tile height in rows */
     uint32_t rank, nranks;      /* this device renders row bands (tiles) of the frame: wo_band_global */
-    uint32_t band_cycle;        /* band weighting: in every band_cycle rounds of the ranks, rank 0 */
-    uint32_t band_skip;         /* sits out band_skip rounds (0: every rank takes one band per round) */
     uint32_t n_recs;            /* program length */
     uint32_t n_prims;           /* primitive count */
     float time_sec;             /* ubershader: UBO time_since_start_sec */
     float sphere_y;             /* ubershader: 2*sin(omega*time), hoisted to the host */
     float inv_width, inv_height; /* path tracer: 1/width, 1/height (fp32); sample position = (x + jitter) * inv_width */
     WoCamera cam;
+    uint32_t band_cycle;        /* band weighting: in every band_cycle rounds of the ranks, rank 0 */
+    uint32_t band_skip;         /* sits out band_skip rounds (0: every rank takes one band per round) */
 } WoFrame;
 
 /* Executed-work counters of a counting launch (wo_renderer_count_work): lane
