@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--no-encode", action="store_true")
     ap.add_argument("--tile-rows", type=int, default=4, help="rows per row-cyclic band (bench.py --tile-rows)")
+    ap.add_argument("--share-streams", type=int, default=2, choices=[1, 2],
+                    help="render streams the other ranks' shares alternate over (2: as rank 0's frames)")
     ap.add_argument("--band", default="auto",
                     help="row-band weighting CYCLE:SKIP (rank 0 sits out SKIP of every CYCLE rounds), 'auto' = "
                          "wololo.default_band(N) as bench.py uses it, '0:0' = a band per rank and round")
@@ -114,7 +116,8 @@ def main():
                 for st in rs:
                     st.wait_event(start)
                 for k in range(F):
-                    r.render_rows_device(p, gather[k & 1][0].data_ptr(), T, rank, n, rs[k & 1].cuda_stream)
+                    st = rs[k & 1] if args.share_streams == 2 else rs[0]
+                    r.render_rows_device(p, gather[k & 1][0].data_ptr(), T, rank, n, st.cuda_stream)
                 for st in rs:
                     main_s.wait_stream(st)
             return go
