@@ -427,6 +427,8 @@ struct LaneTracer {
     const uint32_t* __restrict__ gnode;  // per internal node: left | right << 15 | op << 30
     uint32_t gP, gwords, groot;
     uint64_t gw[kGWin];  // the walk's smallest event keys after `after`, ascending
+    const float4* __restrict__ gclip;  // per primitive: relevance box (LaneBvh::gclip)
+    F3 gri, goi;                       // the ray's reciprocal direction and o * ri (trace_general)
 
     // single-sphere scenes: per ordinal its leaf record, then its material (LaneBvh::leaves)
     const WoRec* __restrict__ lleaf;
@@ -635,8 +637,25 @@ struct LaneTracer {
             return;
         }
 #endif
-        const Ivl iv = prim_ivl(ord, o, d, inv, have_inv);
+        Ivl iv = prim_ivl(ord, o, d, inv, have_inv);
         if constexpr (kGeneral) {
+            // The primitive restricted to its relevance box (build_lbvh): outside it the
+            // primitive cannot change the root (an intersection's other operand, or a
+            // difference's left one, is empty there), so its interval is clipped to the
+            // box's span, widened by a margin past the slab test's rounding.  An end
+            // the clip moves is an event of the clipped primitive that never flips the
+            // root, so the hit -- the first key where the root flips -- is unchanged.
+            if (gclip != nullptr) {
+                const float4 cl = gclip[2u * ord];
+                if (__float_as_uint(cl.w) != 0u) {
+                    float c1;
+                    const float c0 = box_near(cl, gclip[2u * ord + 1u], gri, goi, c1);
+                    const float m0 = __builtin_fmaf(-2e-5f, fabsf(c0), c0) - 1e-5f;
+                    const float m1 = __builtin_fmaf(2e-5f, fabsf(c1), c1) + 1e-5f;
+                    iv.a = fmaxf(iv.a, m0);
+                    iv.b = fminf(iv.b, m1);
+                }
+            }
             if (!(iv.a > iv.b)) {
                 // the first query sets the leaves that hold t_min (the tree's value at
                 // t_min); every query keeps its kGWin smallest keys after `after`, and
@@ -957,6 +976,8 @@ struct LaneTracer {
         const float dz = fabsf(d.z) < 1e-30f ? copysignf(1e-30f, d.z) : d.z;
         const F3 ri = f3(__builtin_amdgcn_rcpf(dx), __builtin_amdgcn_rcpf(dy), __builtin_amdgcn_rcpf(dz));
         const F3 oi = f3(o.x * ri.x, o.y * ri.y, o.z * ri.z);
+        gri = ri;
+        goi = oi;
         F3 inv = f3(0.0f, 0.0f, 0.0f);
         bool have_inv = false;
         for (uint32_t w = 0; w < gwords; ++w) gbits[w * kBlock] = 0u;  // every leaf and node 0
@@ -1010,6 +1031,7 @@ struct LaneBvh {
     // general tree (kind 7): parent per ref, node records, leaves, words per lane, root ref
     const uint32_t* gpar;
     const uint32_t* gnode;
+    const float4* gclip;  // per primitive: relevance box lo (w: 1 = clip) and hi; nullptr: none
     uint32_t gP, gwords, groot;
 };
 
@@ -1073,6 +1095,7 @@ __global__ __launch_bounds__(kBlock, kMode == 14  ? WO_LANES_DYN_TERMS_MIN_WAVES
             tr.gbits = reinterpret_cast<uint32_t*>(top + kNodeF4 * bvh.ntop) + threadIdx.x;
             tr.gpar = bvh.gpar;
             tr.gnode = bvh.gnode;
+            tr.gclip = bvh.gclip;
             tr.gP = bvh.gP;
             tr.gwords = bvh.gwords;
             tr.groot = bvh.groot;
@@ -1346,6 +1369,7 @@ struct WoDev {
     uint32_t lb_terms;     // term mode (kinds 6 / 14): terms the BVH's leaves and always list refer to
     bool lb_general;       // a general tree (kind 7): the BVH over primitives, the tree's tables below
     uint32_t lb_gpar_off, lb_gnode_off;  // u32 offsets in d_lbvh of the parent per ref / node records
+    uint32_t lb_gclip_off;               // u32 offset of the primitives' relevance boxes (0: none)
     uint32_t lb_gP, lb_gwords, lb_groot;  // leaves (= primitives), bit words per lane, the root's ref
     uint32_t last_kind;    // the PathKind of the last path launch (wo_dev_lanes_info)
     uint32_t lb_term_off;  // their records (kTermRecF4 float4 each) at this u32 offset of d_lbvh
@@ -2042,6 +2066,102 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
         }
         prims.push_back(p);
     }
+    // General tree: each primitive's relevance box, the meet of the bounds of the
+    // operands that gate it -- an intersection's other operand, a difference's
+    // left one for its right one -- along its path to the root (outside it the
+    // primitive cannot change the root).  The walk's leaf box becomes the meet of
+    // the primitive's box with it (twice the slack, so the clip's ends lie inside
+    // with room), a primitive whose meet is empty even with the slack never matters
+    // and leaves the walk, and an unbounded primitive with a bounded relevance box
+    // joins the BVH.  visit_leaf clips the primitive's interval to the box's span.
+    std::vector<float4> gclip;
+    if (dev->lb_general) {
+        typedef std::array<double, 6> Box;  // lo xyz, hi xyz
+        const Box inf_box = {-INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, INFINITY};
+        auto meet = [](const Box& x, const Box& y) {
+            Box m;
+            for (int a = 0; a < 3; ++a) {
+                m[a] = fmax(x[a], y[a]);
+                m[3 + a] = fmin(x[3 + a], y[3 + a]);
+            }
+            return m;
+        };
+        auto hull = [](const Box& x, const Box& y) {
+            Box h;
+            for (int a = 0; a < 3; ++a) {
+                h[a] = fmin(x[a], y[a]);
+                h[3 + a] = fmax(x[3 + a], y[3 + a]);
+            }
+            return h;
+        };
+        auto slacked = [](Box x, double k) {
+            for (int a = 0; a < 3; ++a) {
+                if (!std::isfinite(x[a]) || !std::isfinite(x[3 + a])) continue;
+                const double m = k * (1e-4 * (fabs(x[a]) + fabs(x[3 + a]) + fabs(x[3 + a] - x[a])) + 1e-5);
+                x[a] -= m;
+                x[3 + a] += m;
+            }
+            return x;
+        };
+        const uint32_t nref = (uint32_t)gpar.size();
+        std::vector<Box> bnd(nref, inf_box), con(nref, inf_box);
+        for (uint32_t ord = 0; ord < n_prims; ++ord) {
+            double lo[3], hi[3];
+            if (prim_aabb(prog, pc_of[ord], lo, hi)) bnd[ord] = {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]};
+        }
+        for (uint32_t i = 0; i < (uint32_t)gnode.size(); ++i) {  // operands before their node
+            const uint32_t nd = gnode[i], a = nd & kGRefMask, b = (nd >> kGRefBits) & kGRefMask, op = nd >> 30;
+            bnd[n_prims + i] = op == 0u ? hull(bnd[a], bnd[b]) : op == 1u ? meet(bnd[a], bnd[b]) : op == 2u ? bnd[a] : bnd[b];
+        }
+        for (uint32_t i = (uint32_t)gnode.size(); i-- > 0;) {  // a node before its operands
+            const uint32_t nd = gnode[i], a = nd & kGRefMask, b = (nd >> kGRefBits) & kGRefMask, op = nd >> 30;
+            const Box& c = con[n_prims + i];
+            con[a] = op == 1u ? meet(c, bnd[b]) : op == 3u ? meet(c, bnd[b]) : c;  // b AND NOT a: a gated by b
+            con[b] = op == 1u || op == 2u ? meet(c, bnd[a]) : c;                    // a AND NOT b: b gated by a
+        }
+        gclip.assign(2u * n_prims, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+        std::vector<LbPrim> kept;
+        std::vector<uint32_t> alw;
+        size_t clipped = 0, dropped = 0;
+        for (uint32_t ord = 0; ord < n_prims; ++ord) {
+            const Box& c = con[ord];
+            bool bounded = false;
+            for (int a = 0; a < 6; ++a) bounded = bounded || std::isfinite(c[a]);
+            if (bounded) {
+                const Box cs = slacked(c, 1.0);
+                auto fl = [](double v) { return (float)fmax(-1e30, fmin(1e30, v)); };
+                gclip[2u * ord] = make_float4(fl(cs[0]), fl(cs[1]), fl(cs[2]), 1.0f);  // w != 0: clip
+                gclip[2u * ord + 1u] = make_float4(fl(cs[3]), fl(cs[4]), fl(cs[5]), 0.0f);
+                ++clipped;
+            }
+            const Box m = meet(slacked(bnd[ord], 2.0), slacked(c, 2.0));
+            bool empty = false, finite = true;
+            for (int a = 0; a < 3; ++a) {
+                empty = empty || m[a] > m[3 + a];
+                finite = finite && std::isfinite(m[a]) && std::isfinite(m[3 + a]);
+            }
+            if (empty) {
+                ++dropped;
+                continue;  // never matters: its bit stays 0
+            }
+            if (!finite) {
+                alw.push_back(ord);
+                continue;
+            }
+            LbPrim p;
+            p.ord = ord;
+            for (int a = 0; a < 3; ++a) {
+                p.lo[a] = m[a];
+                p.hi[a] = m[3 + a];
+                p.c[a] = 0.5 * (p.lo[a] + p.hi[a]);
+            }
+            kept.push_back(p);
+        }
+        prims.swap(kept);
+        always.swap(alw);
+        if (!clipped) gclip.clear();
+        (void)dropped;
+    }
     if (!prims.empty()) {
         std::vector<double> diag(prims.size());
         for (size_t i = 0; i < prims.size(); ++i) {
@@ -2160,9 +2280,11 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     dev->lb_leaf_off = dev->lb_spheres_only ? (uint32_t)(leaf_off / sizeof(uint32_t)) : 0u;
     const size_t gpar_off = leaf_off + (dev->lb_spheres_only ? (size_t)n_prims * 2u * sizeof(WoRec) : 0u);
     const size_t gnode_off = gpar_off + gpar.size() * sizeof(uint32_t);
-    const size_t bytes = gnode_off + gnode.size() * sizeof(uint32_t);
+    const size_t gclip_off = (gnode_off + gnode.size() * sizeof(uint32_t) + 15u) & ~(size_t)15u;
+    const size_t bytes = gclip_off + gclip.size() * sizeof(float4);
     dev->lb_gpar_off = (uint32_t)(gpar_off / sizeof(uint32_t));
     dev->lb_gnode_off = (uint32_t)(gnode_off / sizeof(uint32_t));
+    dev->lb_gclip_off = gclip.empty() ? 0u : (uint32_t)(gclip_off / sizeof(uint32_t));
     dev->lb_gP = n_prims;
     dev->lb_gwords = (uint32_t)((gpar.size() + 31u) / 32u);
     dev->lb_groot = groot;
@@ -2170,6 +2292,7 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
     std::vector<char> blob(bytes);
     if (!gpar.empty()) memcpy(blob.data() + gpar_off, gpar.data(), gpar.size() * sizeof(uint32_t));
     if (!gnode.empty()) memcpy(blob.data() + gnode_off, gnode.data(), gnode.size() * sizeof(uint32_t));
+    if (!gclip.empty()) memcpy(blob.data() + gclip_off, gclip.data(), gclip.size() * sizeof(float4));
     if (dev->lb_spheres_only)
         for (uint32_t ord = 0; ord < n_prims; ++ord) {
             const WoRec& L = prog[pc_of[ord] + 1u];
@@ -2211,6 +2334,9 @@ static LaneBvh lane_bvh(const WoDev* dev) {
                                 : nullptr;
     b.gpar = reinterpret_cast<const uint32_t*>(dev->d_lbvh) + dev->lb_gpar_off;
     b.gnode = reinterpret_cast<const uint32_t*>(dev->d_lbvh) + dev->lb_gnode_off;
+    b.gclip = dev->lb_gclip_off ? reinterpret_cast<const float4*>(reinterpret_cast<const uint32_t*>(dev->d_lbvh) +
+                                                                 dev->lb_gclip_off)
+                                : nullptr;
     b.gP = dev->lb_gP;
     b.gwords = dev->lb_gwords;
     b.groot = dev->lb_groot;
