@@ -1535,11 +1535,11 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * LDS within the CU (csg32 5.24 -> 5.19 ms; csg256 balanced keeps 8 entries:
      * 15.12 vs 15.33 ms at 7) */
     if (g.lds_events && n_prims <= 64u) bput(&b, "#ifndef WO_LDS_EVENTS\n#define WO_LDS_EVENTS 7\n#endif\n");
-    /* The take's job ring (pathtrace_block) costs 8 KB of LDS per workgroup: with an
-     * LDS event list beside it the workgroups no longer fit (csg256 balanced 9.26 ->
-     * 12.13 ms, csg32_nested 10.66 -> 11.79); term mode and the register window keep
-     * it (csg32 3.13 -> 3.07, chain 12.86 -> 12.77). */
-    if (g.lds_events && !g.term_mode) bput(&b, "#ifndef WO_TAKE_RING\n#define WO_TAKE_RING 0\n#endif\n");
+    /* The take's job ring (pathtrace_block) costs 8 KB of LDS per workgroup: term mode
+     * and the register window use it (csg32 3.13 -> 3.07 ms, chain 12.86 -> 12.77);
+     * beside an LDS event list the workgroups no longer fit (csg256 balanced 9.26 ->
+     * 12.13 ms, csg32_nested 10.66 -> 11.79). */
+    bput(&b, "#ifndef WO_TAKE_RING\n#define WO_TAKE_RING %d\n#endif\n", !(g.lds_events && !g.term_mode));
     bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
          g.lds_events && !g.term_mode, tree_depth(prog, n_recs), lds_prog);
     if (n_uterms) {
