@@ -722,6 +722,11 @@ int wo_renderer_set_band_weight(Wo_Renderer* r, uint32_t band_cycle, uint32_t ba
         wo_set_error("band weight: skip %u must be below the cycle %u (or 0)", band_skip, band_cycle);
         return -1;
     }
+    /* the band arithmetic forms cycle * nranks (<= 16 ranks) in 32 bits */
+    if (band_skip != 0u && band_cycle > WO_BAND_CYCLE_MAX) {
+        wo_set_error("band weight: cycle %u exceeds %u", band_cycle, (unsigned)WO_BAND_CYCLE_MAX);
+        return -1;
+    }
     r->band_cycle = band_skip ? band_cycle : 0u;
     r->band_skip = band_skip;
     return 0;
@@ -865,10 +870,12 @@ float const* wo_renderer_last_frame(Wo_Renderer* r, uint32_t* width, uint32_t* h
     if (!r->last_frame && r->last_bgra8 && r->dev && r->last_slot >= 0) {
         char err[256] = {0};
         float const* px = NULL;
+        const int cur = wo_dev_current(); /* the map selects the root's device: restore the caller's */
         if (wo_dev_frame_map_float(r->dev, r->last_slot, &px, err, sizeof err) == 0)
             r->last_frame = px;
         else
             wo_set_error("last frame: %s", err);
+        if (cur >= 0) (void)wo_dev_select(cur);
     }
     if (width) *width = r->last_frame ? r->last_w : 0u;
     if (height) *height = r->last_frame ? r->last_h : 0u;

@@ -1540,6 +1540,12 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * beside an LDS event list the workgroups no longer fit (csg256 balanced 9.26 ->
      * 12.13 ms, csg32_nested 10.66 -> 11.79). */
     bput(&b, "#ifndef WO_TAKE_RING\n#define WO_TAKE_RING %d\n#endif\n", !(g.lds_events && !g.term_mode));
+    /* Camera-ray waves (pathtrace_block): camera rays traced in iterations of their
+     * own, so a wave's culling sees coherent rays (csg32 3.125 -> 2.80 ms, chain 12.74
+     * -> 11.35).  Their ring of ready paths (12 KB per workgroup) does not fit beside
+     * an LDS event list at 8 workgroups per CU (csg32_nested 10.55 -> 11.76, csg256
+     * balanced 9.30 -> 10.59 at 4 waves per SIMD). */
+    bput(&b, "#ifndef WO_CAM_WAVES\n#define WO_CAM_WAVES %d\n#endif\n", !(g.lds_events && !g.term_mode));
     bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
          g.lds_events && !g.term_mode, tree_depth(prog, n_recs), lds_prog);
     if (n_uterms) {

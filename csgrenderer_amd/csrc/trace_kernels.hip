@@ -1397,6 +1397,10 @@ struct WoDev {
     // the D2H copies run on their own stream, gated by rend_ev (the slot's frame is
     // rendered), so the next frame's kernel starts as soon as this one ends.
     hipStream_t copy_stream;
+    // On-demand float map-back of a presented frame (wo_dev_frame_map_float): its own
+    // stream, created on first use, so it never queues behind the next frame's
+    // map-back on copy_stream (which waits for that frame's render).
+    hipStream_t map_stream;
     hipEvent_t rend_ev[WO_SLOTS];
     bool slot_float[WO_SLOTS];  // the float frame was copied with the last map-back
     size_t slot_pixels[WO_SLOTS];  // pixels of the slot's last frame
@@ -1535,6 +1539,7 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
     if (dev->st_base) (void)hipEventDestroy(dev->st_base);
     if (dev->jit_module) (void)hipModuleUnload(dev->jit_module);
     if (dev->count_module) (void)hipModuleUnload(dev->count_module);
+    if (dev->map_stream) (void)hipStreamDestroy(dev->map_stream);
     (void)hipStreamDestroy(dev->copy_stream);
     (void)hipStreamDestroy(dev->stream);
     delete dev;
@@ -3225,11 +3230,16 @@ extern "C" int wo_dev_frame_map_float(WoDev* dev, int slot, float const** host, 
         return -1;
     }
     if (!dev->slot_float[slot]) {
+        // The presented slot's frame is complete (its slot_ev was waited for when it
+        // was presented); the copy runs on map_stream, after slot_ev, so it does not
+        // wait for the frame in flight behind it on copy_stream.
         hipError_t e = hipSetDevice(dev->device);
         const size_t bytes = dev->slot_pixels[slot] * sizeof(float4);
+        if (e == hipSuccess && !dev->map_stream) e = hipStreamCreateWithFlags(&dev->map_stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamWaitEvent(dev->map_stream, dev->slot_ev[slot], 0);
         if (e == hipSuccess) e = hipMemcpyAsync(dev->h_slot[slot], dev->d_slot[slot], bytes, hipMemcpyDeviceToHost,
-                                                dev->copy_stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(dev->copy_stream);
+                                                dev->map_stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(dev->map_stream);
         if (e != hipSuccess) {
             set_err(err, errlen, "float frame map-back", e);
             return -1;

@@ -532,8 +532,11 @@ def jit_compile_check(src: str, arch: str = "gfx950") -> str:
     return "" if rc == 0 else err.value.decode(errors="replace")
 
 
+BAND_CYCLE_MAX = 65536  # wo_scene.h WO_BAND_CYCLE_MAX
+
+
 def _weighted(nranks, band):
-    return nranks >= 2 and 0 < band[1] < band[0]
+    return nranks >= 2 and 0 < band[1] < band[0] <= BAND_CYCLE_MAX
 
 
 def band_global(lb: int, rank: int, nranks: int, band=(0, 0)) -> int:

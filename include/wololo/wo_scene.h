@@ -152,8 +152,10 @@ enum {
  * `skip` rounds one to every rank but 0 -- rank 0, which also gathers, assembles
  * and presents the frame, renders (cycle - skip) / cycle of another rank's share.
  * (Mirrored by wo_device_common.h local_to_global_row and wololo.py global_row.) */
+/* cycles longer than this are not weighted (cycle * n stays far inside 32 bits) */
+#define WO_BAND_CYCLE_MAX 65536u
 static inline int wo_band_weighted(uint32_t n, uint32_t cycle, uint32_t skip) {
-    return n >= 2u && skip > 0u && skip < cycle;
+    return n >= 2u && skip > 0u && skip < cycle && cycle <= WO_BAND_CYCLE_MAX;
 }
 /* the frame band of rank `rank`'s local band lb */
 static inline uint32_t wo_band_global(uint32_t lb, uint32_t rank, uint32_t n, uint32_t cycle, uint32_t skip) {
