@@ -483,7 +483,8 @@ def report_line(args, r, info, params, world, elapsed_s, segs_all, segs_local, k
     cpu = None
     if world == 1 and not args.no_cpu_baseline and info.mode == wl.MODE_PATHTRACE:
         cpu = cpu_baseline(r, params, args.cpu_seconds)
-    cfg = {"workload": f"{info.name}: {W}x{H}, {params.spp} spp, {params.max_depth} bounces, "
+    shape = f" ({info.shape})" if info.shape else ""
+    cfg = {"workload": f"{info.name}{shape}: {W}x{H}, {params.spp} spp, {params.max_depth} bounces, "
                        f"{info.spheres} spheres + {info.halfspaces} half-spaces, {info.binops} binops",
            "scene": info.name, "width": W, "height": H, "spp": params.spp,
            "max_depth": params.max_depth, "tile_rows": T}

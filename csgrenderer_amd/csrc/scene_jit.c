@@ -503,12 +503,13 @@ static void gen_collect_terms(Gen* g, int indent) {
  * divergent sweep loop is not provably so: the first lane's copy (exact) puts it
  * in an SGPR for the move. */
 static void gen_cull_barrier(Gen* g, int indent) {
-    if (!g->cull_barrier) return;
+    bput(g->b, "#if WO_JIT_CULL_BARRIER\n");
     for (uint32_t w = 0; w < g->ncw; ++w)
         bput(g->b,
              "%*s{ uint32_t cw = (uint32_t)__builtin_amdgcn_readfirstlane((int)cull[%u]); "
              "asm volatile(\"\" : \"+s\"(cw)); cull[%u] = cw; }\n",
              indent, "", w, w);
+    bput(g->b, "#endif\n");
 }
 
 /* the collect of the whole program (either pass) */
@@ -1322,6 +1323,128 @@ static void gen_union_sweep(Gen* g, const UTerm* uterms, uint32_t n_uterms, uint
          "};\n");
 }
 
+/* ---- root evaluation by truth tables ----
+ * A small general tree (no union count, no term mode) splits into K <= 4
+ * subtrees of <= 12 primitives each, every one a contiguous ordinal range
+ * (postfix order numbers a subtree's primitives consecutively).  A subtree's
+ * value is one bit of its truth table (2^n bits, indexed by its range of the
+ * membership words) and the root one bit of a 2^K-entry table over the K
+ * subtree values: per event K table reads from LDS and a shift, instead of the
+ * tree's masked compares and lane-mask operations (csg32_nested: two subtrees of
+ * 9 and 10 primitives). */
+#define LUT_MAX_BITS 12u
+#define LUT_MAX_SUBS 4u
+typedef struct TNode {
+    int op; /* 0 primitive, else WO_OP_UNION / _INTER / _DIFF / _RDIFF */
+    int l, r;
+    uint32_t lo, n; /* ordinal range [lo, lo + n) */
+} TNode;
+
+typedef struct LutPlan {
+    uint32_t k;                    /* subtrees */
+    uint32_t lo[LUT_MAX_SUBS], n[LUT_MAX_SUBS], off[LUT_MAX_SUBS];
+    int node[LUT_MAX_SUBS];
+    uint32_t words;                /* table words in all */
+    uint32_t top;                  /* bit j: the root when subtree s has value (j >> s) & 1 */
+    uint32_t* table;
+} LutPlan;
+
+static int tn_eval(const TNode* t, int x, uint32_t lo, uint32_t idx, const LutPlan* pl, uint32_t j) {
+    if (pl) /* a subtree of the plan: its value from j */
+        for (uint32_t s = 0; s < pl->k; ++s)
+            if (pl->node[s] == x) return (int)((j >> s) & 1u);
+    const TNode* n = &t[x];
+    if (n->op == 0) return (int)((idx >> (n->lo - lo)) & 1u);
+    const int a = tn_eval(t, n->l, lo, idx, pl, j), b = tn_eval(t, n->r, lo, idx, pl, j);
+    return n->op == WO_OP_UNION ? (a | b) : n->op == WO_OP_INTER ? (a & b) : n->op == WO_OP_DIFF ? (a & !b) : (b & !a);
+}
+
+static int lut_split(const TNode* t, int x, LutPlan* pl) {
+    if (t[x].n <= LUT_MAX_BITS) {
+        if (pl->k == LUT_MAX_SUBS) return 0;
+        pl->node[pl->k] = x;
+        pl->lo[pl->k] = t[x].lo;
+        pl->n[pl->k] = t[x].n;
+        ++pl->k;
+        return 1;
+    }
+    return lut_split(t, t[x].l, pl) && lut_split(t, t[x].r, pl);
+}
+
+/* 1 with *pl filled (pl->table malloc'd), 0 when the tree does not split so */
+static int lut_plan(const WoRec* prog, uint32_t n_recs, uint32_t n_prims, LutPlan* pl) {
+    memset(pl, 0, sizeof *pl);
+    if (n_prims == 0u || n_prims > 64u) return 0;
+    TNode* t = (TNode*)malloc(sizeof(TNode) * (2u * n_prims));
+    int* st = (int*)malloc(sizeof(int) * (n_prims + 1u));
+    uint32_t nt = 0, sp = 0;
+    int ok = t && st;
+    for (uint32_t pc = 0; pc < n_recs && ok;) {
+        const WoRec* r = &prog[pc];
+        if (r->op == WO_OP_PRIM) {
+            ok = nt < 2u * n_prims && sp <= n_prims;
+            if (!ok) break;
+            TNode x = {0, -1, -1, r->u1, 1u};
+            t[nt] = x;
+            st[sp++] = (int)nt++;
+            pc += 1u + r->u0;
+            continue;
+        }
+        ++pc;
+        if (r->op == WO_OP_BOUND) continue;
+        ok = sp >= 2u && nt < 2u * n_prims;
+        if (!ok) break;
+        const int b = st[--sp], a = st[--sp];
+        TNode x = {(int)r->op, a, b, t[a].lo < t[b].lo ? t[a].lo : t[b].lo, t[a].n + t[b].n};
+        ok = t[a].lo + t[a].n == t[b].lo || t[b].lo + t[b].n == t[a].lo; /* contiguous ranges */
+        t[nt] = x;
+        st[sp++] = (int)nt++;
+    }
+    ok = ok && sp == 1u && t[st[0]].lo == 0u && t[st[0]].n == n_prims && lut_split(t, st[0], pl) && pl->k >= 1u;
+    for (uint32_t s = 0; ok && s < pl->k; ++s) {
+        ok = (pl->lo[s] % 32u) + pl->n[s] <= 64u && pl->lo[s] / 32u + ((pl->lo[s] % 32u) + pl->n[s] > 32u) < 2u;
+        pl->off[s] = pl->words;
+        pl->words += pl->n[s] >= 5u ? 1u << (pl->n[s] - 5u) : 1u;
+    }
+    if (ok) {
+        pl->table = (uint32_t*)calloc(pl->words, sizeof(uint32_t));
+        ok = pl->table != NULL;
+    }
+    for (uint32_t s = 0; ok && s < pl->k; ++s)
+        for (uint32_t idx = 0; idx < (1u << pl->n[s]); ++idx)
+            if (tn_eval(t, pl->node[s], pl->lo[s], idx, NULL, 0u)) pl->table[pl->off[s] + (idx >> 5)] |= 1u << (idx & 31u);
+    for (uint32_t j = 0; ok && j < (1u << pl->k); ++j)
+        if (tn_eval(t, st[0], 0u, 0u, pl, j)) pl->top |= 1u << j;
+    free(t);
+    free(st);
+    if (!ok) {
+        free(pl->table);
+        memset(pl, 0, sizeof *pl);
+    }
+    return ok;
+}
+
+/* the root's value r from bits[] through the tables (WO_LUT: the LDS copy) */
+static void lut_emit_eval(Buf* b, const LutPlan* pl, int indent) {
+    bput(b, "%*suint32_t lsub = 0u;\n", indent, "");
+    for (uint32_t s = 0; s < pl->k; ++s) {
+        const uint32_t w = pl->lo[s] / 32u, sh = pl->lo[s] % 32u, n = pl->n[s];
+        char idx[160];
+        if (sh + n <= 32u)
+            snprintf(idx, sizeof idx, "(bits[%u] >> %u) & 0x%xu", w, sh, (1u << n) - 1u);
+        else
+            snprintf(idx, sizeof idx, "(uint32_t)((((uint64_t)bits[%u] << 32) | bits[%u]) >> %u) & 0x%xu", w + 1u, w, sh,
+                     (1u << n) - 1u);
+        if (n >= 5u)
+            bput(b, "%*s{ const uint32_t i = %s; lsub |= ((WO_LUT[%uu + (i >> 5)] >> (i & 31u)) & 1u) << %u; }\n",
+                 indent, "", idx, pl->off[s], s);
+        else
+            bput(b, "%*s{ const uint32_t i = %s; lsub |= ((0x%08xu >> i) & 1u) << %u; }\n", indent, "", idx,
+                 pl->table[pl->off[s]], s);
+    }
+    bput(b, "%*sr = (0x%08xu >> lsub) & 1u;  // the root from the %u subtree values\n", indent, "", pl->top, pl->k);
+}
+
 char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prims) {
     Buf b = {0};
     Gen g;
@@ -1517,6 +1640,15 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         else n_uterms = union_terms(prog, n_recs, n_prims, uterms, n_prims);
         if (n_uterms < 8u) n_uterms = 0;
     }
+    /* truth-table root evaluation for the general form (lut_plan) */
+    LutPlan lut;
+    memset(&lut, 0, sizeof lut);
+    const int use_lut = n_prims && !g.term_mode && !n_uterms && lut_plan(prog, n_recs, n_prims, &lut);
+    if (use_lut) {
+        bput(&b, "#ifndef WO_JIT_LUT\n#define WO_JIT_LUT 1\n#endif\n");
+    } else {
+        bput(&b, "#define WO_JIT_LUT 0\n");
+    }
     /* A full LDS event list keeps its smallest keys (WO_LDS_KEEP_SMALLEST): csg32_nested
      * 20.18 -> 10.97 ms (re-collects per segment 0.86 -> 0.18).  A union of small
      * terms (csg32, csg256 balanced) rarely fills the list, and there the eviction
@@ -1526,10 +1658,19 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * 13.21 ms, balanced 9.70 -> 9.47, csg32 3.273 -> 3.238), except for a general
      * root evaluation over the LDS event list (csg32_nested 10.92 -> 11.75: its SGPR
      * spills became 564 spilled VGPRs) */
-    g.cull_barrier = !(g.lds_events && !n_uterms && !g.term_mode);
+    /* (off for the LDS event list's general evaluation: csg32_nested's SGPR spills
+     * became 564 spilled VGPRs, 10.92 -> 11.75 ms; with the register window and the
+     * truth tables it helps: 9.33 -> 9.26) */
+    g.cull_barrier = 1;
+    bput(&b, "#ifndef WO_JIT_CULL_BARRIER\n#define WO_JIT_CULL_BARRIER %d\n#endif\n", g.cull_barrier);
     /* the register window for deep trees holds 5 events (csg256 chain 29.5 ms at 4,
      * 27.6 at 6, 27.5 at 8; with decision lists 19.36 at 4, 18.47 at 5, 18.65 at 6) */
-    if (!g.lds_events) bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW 5\n#endif\n");
+    /* The register window's events: 5 for deep trees (csg256 chain 29.5 ms at 4, 27.6 at 6,
+     * 27.5 at 8; with decision lists 19.36 at 4, 18.47 at 5, 18.65 at 6); the union count
+     * (csg256 balanced 9.98 / 9.32 / 10.00 ms at 4 / 5 / 6); 8 for the truth-table form
+     * (csg32_nested 9.64 / 9.33 / 9.07 at 4 / 5 / 6, with the cull barrier 9.01 / 8.91 / 8.89
+     * at 6 / 7 / 8). */
+    bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW %d\n#endif\n", use_lut ? 8 : 5);
     if (g.term_mode) bput(&b, "// term mode: %u terms (%u outside the spatial hierarchy)\n", n_jterms, g.ntunb);
     /* small scenes run 8 waves per SIMD: a 7-entry LDS list keeps 8 workgroups'
      * LDS within the CU (csg32 5.24 -> 5.19 ms; csg256 balanced keeps 8 entries:
@@ -1539,15 +1680,24 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * and the register window use it (csg32 3.13 -> 3.07 ms, chain 12.86 -> 12.77);
      * beside an LDS event list the workgroups no longer fit (csg256 balanced 9.26 ->
      * 12.13 ms, csg32_nested 10.66 -> 11.79). */
-    bput(&b, "#ifndef WO_TAKE_RING\n#define WO_TAKE_RING %d\n#endif\n", !(g.lds_events && !g.term_mode));
+    bput(&b, "#ifndef WO_TAKE_RING\n#define WO_TAKE_RING 1\n#endif\n");
     /* Camera-ray waves (pathtrace_block): camera rays traced in iterations of their
      * own, so a wave's culling sees coherent rays (csg32 3.125 -> 2.80 ms, chain 12.74
      * -> 11.35).  Their ring of ready paths (12 KB per workgroup) does not fit beside
      * an LDS event list at 8 workgroups per CU (csg32_nested 10.55 -> 11.76, csg256
      * balanced 9.30 -> 10.59 at 4 waves per SIMD). */
-    bput(&b, "#ifndef WO_CAM_WAVES\n#define WO_CAM_WAVES %d\n#endif\n", !(g.lds_events && !g.term_mode));
-    bput(&b, "#include \"wo_device_common.h\"\n#define WO_JIT_LDS_EVENTS %d  // tree depth %u\n#define WO_JIT_LDS_PROG %d\n\n",
-         g.lds_events && !g.term_mode, tree_depth(prog, n_recs), lds_prog);
+    bput(&b, "#ifndef WO_CAM_WAVES\n#define WO_CAM_WAVES 1\n#endif\n");
+    /* WO_JIT_LDS_EVENTS=0 (WOLOLO_JIT_FLAGS) puts a small tree's event window in
+     * registers (wodev::Window) instead of the LDS list */
+    bput(&b, "#include \"wo_device_common.h\"\n#ifndef WO_JIT_LDS_EVENTS\n#define WO_JIT_LDS_EVENTS 0  // tree depth %u\n#endif\n#define WO_JIT_LDS_PROG %d\n\n",
+         tree_depth(prog, n_recs), lds_prog);
+    if (use_lut) {
+        bput(&b, "// root by truth tables: %u subtrees (", lut.k);
+        for (uint32_t s2 = 0; s2 < lut.k; ++s2) bput(&b, "%s[%u, %u)", s2 ? ", " : "", lut.lo[s2], lut.lo[s2] + lut.n[s2]);
+        bput(&b, ")\n__constant__ uint32_t kLut[%u] = {", lut.words);
+        for (uint32_t i = 0; i < lut.words; ++i) bput(&b, "%s0x%08xu", i ? ", " : "", lut.table[i]);
+        bput(&b, "};\n");
+    }
     if (n_uterms) {
         bput(&b, "struct __attribute__((aligned(16))) WoUTerm { uint64_t m, q; uint32_t w, neg, pad0, pad1; };\n");
         bput(&b, "// root = union of %u literal-set terms: a term is true iff ((window(w) & m) == q) != neg,\n"
@@ -1583,6 +1733,10 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "  const WoRec* __restrict__ prog;\n"
          "  const uint32_t* __restrict__ ordpc;\n"
          "  uint64_t* ev;  // LDS event list column (LdsWindow)\n"
+         "#if WO_JIT_LUT\n"
+         "  const __attribute__((address_space(3))) uint32_t* lut;  // LDS copy of kLut\n"
+         "#define WO_LUT lut\n"
+         "#endif\n"
          "  __device__ __forceinline__ WoRec hit_leaf(const wodev::Hit& h) const {\n"
          "    return prog[ordpc[h.ord] + 1u + h.member];\n"
          "  }\n"
@@ -1650,13 +1804,15 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          * the re-collect copy (events after the last processed one, when the
          * window had dropped some) is separate code so the common pass carries
          * none of its tests. */
+        if (g.lds_events)
+            bput(&b, "#if WO_JIT_LDS_EVENTS\n    wodev::LdsWindow win; win.ev = ev; win.clear();\n"
+                     "#else\n    wodev::Window win; win.clear();\n#endif\n");
+        else
+            bput(&b, "    wodev::Window win; win.clear();\n");
         bput(&b,
-             "    %s win; %swin.clear();\n"
              "    uint64_t after = 0ull, key = 0ull;\n"
              "    WO_MARK(\"collect_begin\");\n"
-             "    {\n",
-             !g.lds_events ? "wodev::Window" : "wodev::LdsWindow",
-             !g.lds_events ? "" : "win.ev = ev; ");
+             "    {\n");
         g.first_pass = 1;
         gen_collect_all(&g, 6);
         bput(&b,
@@ -1705,8 +1861,12 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  "      uint32_t r;\n");
             bput(&b,
                  "      // WO_EVAL_BEGIN (the root's value from bits[] and cull[]; tests/test_jit.py compiles it on the host)\n"
-                 "      {\n");
+                 "%s      {\n", use_lut ? "#if WO_JIT_LUT\n" : "");
             g.nbound = 0;
+            if (use_lut) {
+                lut_emit_eval(&b, &lut, 8);
+                bput(&b, "      }\n#else\n      {\n");
+            }
             {
                 Term rt = gen_eval_flat(&g, 0, n_recs, 8);
                 const uint32_t m = rt.kind ? (rt.P | rt.N) : 0u;
@@ -1714,6 +1874,10 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                                                                                  : rt.cost + (m ? 3u : 0u);
                 uint32_t rv = term_name(&g, &rt, 8);
                 bput(&b, "        r = v%u ? 1u : 0u;\n      }\n", rv);
+            }
+            if (use_lut) {
+                bput(&b, "#endif\n");
+                eval_ops = 6u * lut.k + 2u; /* per subtree: index, address, read, bit; the root's shift */
             }
             bput(&b, "      // WO_EVAL_END\n");
             bput(&b,
@@ -1767,6 +1931,11 @@ kernel_tail:
          "#else\n"
          "  tr.ev = nullptr;\n"
          "#endif\n"
+         "#if WO_JIT_LUT\n"
+         "  __shared__ uint32_t s_lut[sizeof(kLut) / 4];\n"
+         "  for (uint32_t i = threadIdx.x; i < sizeof(kLut) / 4; i += wodev::kBlock) s_lut[i] = kLut[i];\n"
+         "  tr.lut = (const __attribute__((address_space(3))) uint32_t*)s_lut;\n"
+         "#endif\n"
          "#if WO_JIT_LDS_PROG  // hit-leaf and material reads from LDS (pathtrace_block's first barrier orders the copy)\n"
          "  __shared__ WoRec s_prog[%u];\n"
          "  __shared__ WoMaterial s_mats[%u];\n"
@@ -1791,6 +1960,7 @@ kernel_tail:
      * executed-work roofline (0: not known, e.g. the postfix form) */
     if (eval_ops) bput(&b, "// wo_eval_ops_per_event %u\n", eval_ops);
     free(g.dls);
+    free(lut.table);
     free(uterms);
     free(sprims);
     free(tunb);

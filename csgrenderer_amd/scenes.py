@@ -61,6 +61,7 @@ class SceneInfo:
     spp: int
     max_depth: int
     mode: int = MODE_PATHTRACE
+    shape: str = ""  # the CSG tree's shape, for the bench line's workload label
 
     @property
     def leaves(self) -> int:
@@ -230,7 +231,8 @@ def build_csg32(r: Renderer, seed: int = 32, width=1920, height=1080, spp=64, un
     r.union(arg(objs), arg(rest, roff))
     r.set_camera((0.0, 4.5, 10.0), (0.0, 0.6, 0.0), (0, 1, 0), 45.0, 0.0, 10.0)
     return SceneInfo("csg32_union" if union_only else "csg32", spheres=20, halfspaces=12, binops=31, width=width, height=height, spp=spp,
-                     max_depth=8)
+                     max_depth=8,
+                     shape="root union of 14 terms of <= 2 literals" if not union_only else "union of primitives")
 
 
 class NestedShape:
@@ -331,7 +333,8 @@ def build_csg32_nested(r: Renderer, seed: int = 3235, width=1920, height=1080, s
     nb = len(box_at)
     name = "csg32_nested" if n_items == 22 else f"csg{n_items}_nested"
     return SceneInfo(name, spheres=n_items - nb, halfspaces=6 * nb, binops=n_items - 1 + 5 * nb, width=width,
-                     height=height, spp=spp, max_depth=8)
+                     height=height, spp=spp, max_depth=8,
+                     shape="one balanced tree, intersections and differences at every level")
 
 
 def build_csg256(r: Renderer, seed: int = 256, shape: str = "balanced", width=1920, height=1080,

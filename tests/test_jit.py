@@ -318,10 +318,10 @@ def _union_of_pairs(r, n, seed):
     return items[0]
 
 
-def _compile_sweep(tmp_path, src, nw, ncull):
-    """The generated evaluation and toggle blocks (and the union-count table) as a
-    host function: evaluate at the start membership, then apply toggles, writing
-    the root after each."""
+def _compile_sweep(tmp_path, src, nw, ncull, lut=1):
+    """The generated evaluation and toggle blocks (and the union-count table, or the
+    truth tables with WO_JIT_LUT=`lut`) as a host function: evaluate at the start
+    membership, then apply toggles, writing the root after each."""
     import ctypes
     import subprocess
 
@@ -334,8 +334,12 @@ def _compile_sweep(tmp_path, src, nw, ncull):
         table = (m.group(0) + "\n" + t.group(0).replace("__constant__", "static const") + "\n"
                  "#define WO_UTERM kUTerm\n")
         assert "ucnt" in toggle
-    root_after = "(ucnt != 0)" if table else None
-    c = tmp_path / "ev.cpp"
+    m = re.search(r"__constant__ uint32_t kLut\[\d+\] = \{.*?\};", src, re.S)
+    if m:
+        table += m.group(0).replace("__constant__", "static const") + "\n#define WO_LUT kLut\n"
+    table = f"#define WO_JIT_LUT {lut}\n" + table
+    root_after = "(ucnt != 0)" if "kUTerm" in table else None
+    c = tmp_path / f"ev{lut}.cpp"
     c.write_text("#include <stddef.h>\n#include <stdint.h>\n" + table +
                  "extern \"C\" void run(const uint32_t* all, int n, const uint32_t* ords, int nev, uint32_t* out) {\n"
                  f"  for (int i = 0; i < n; ++i) {{\n    uint32_t bits[{nw}];\n"
@@ -346,10 +350,10 @@ def _compile_sweep(tmp_path, src, nw, ncull):
                  "      const uint64_t key = (uint64_t)ords[(size_t)i * nev + e] << 12;\n" + toggle +
                  ("      out[(size_t)i * (nev + 1) + e + 1] = " + (root_after or "0") + ";\n") +
                  "    }\n  }\n}\n")
-    so = tmp_path / "ev.so"
+    so = tmp_path / f"ev{lut}.so"
     subprocess.run(["g++", "-O1", "-shared", "-fPIC", "-o", str(so), str(c)], check=True)
     lib = ctypes.CDLL(str(so))
-    return lib, table != ""
+    return lib, root_after is not None
 
 
 @pytest.mark.parametrize("case", ["csg32_nested", "csg256_balanced", "csg256_chain", "chain_uud", "chain_uid",
@@ -375,9 +379,19 @@ def test_generated_root_evaluation(hostonly, tmp_path, case):
     if case in ("csg256_balanced", "unionpairs"):
         assert "kUTerm" in src  # a union of >= 12 literal-set terms: the incremental count
         assert wl.jit_compile_check(src, "gfx950") == ""
+    if case == "csg32_nested":
+        assert "kLut" in src  # two subtrees of <= 12 primitives: the truth-table evaluation
+        assert wl.jit_compile_check(src, "gfx950") == ""
+    for lut in ((1, 0) if "kLut" in src else (1,)):
+        _check_generated_eval(tmp_path, src, prog, nrec, nprim, lut)
+
+
+def _check_generated_eval(tmp_path, src, prog, nrec, nprim, lut):
+    import ctypes
+
     nw = (nprim + 31) // 32
     ncull = max(1, len(re.findall(r"cull\[(\d+)\] = 0u;", src)))
-    lib, counted = _compile_sweep(tmp_path, src, nw, ncull)
+    lib, counted = _compile_sweep(tmp_path, src, nw, ncull, lut)
     rng = np.random.default_rng(7)
     rows = [np.eye(nprim, dtype=np.uint8), np.zeros((1, nprim), dtype=np.uint8)]  # every primitive alone
     for p in (0.01, 0.03, 0.1, 0.3, 0.5):
