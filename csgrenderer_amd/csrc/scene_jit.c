@@ -1676,16 +1676,13 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * LDS within the CU (csg32 5.24 -> 5.19 ms; csg256 balanced keeps 8 entries:
      * 15.12 vs 15.33 ms at 7) */
     if (g.lds_events && n_prims <= 64u) bput(&b, "#ifndef WO_LDS_EVENTS\n#define WO_LDS_EVENTS 7\n#endif\n");
-    /* The take's job ring (pathtrace_block) costs 8 KB of LDS per workgroup: term mode
-     * and the register window use it (csg32 3.13 -> 3.07 ms, chain 12.86 -> 12.77);
-     * beside an LDS event list the workgroups no longer fit (csg256 balanced 9.26 ->
-     * 12.13 ms, csg32_nested 10.66 -> 11.79). */
-    bput(&b, "#ifndef WO_TAKE_RING\n#define WO_TAKE_RING 1\n#endif\n");
     /* Camera-ray waves (pathtrace_block): camera rays traced in iterations of their
      * own, so a wave's culling sees coherent rays (csg32 3.125 -> 2.80 ms, chain 12.74
-     * -> 11.35).  Their ring of ready paths (12 KB per workgroup) does not fit beside
-     * an LDS event list at 8 workgroups per CU (csg32_nested 10.55 -> 11.76, csg256
-     * balanced 9.30 -> 10.59 at 4 waves per SIMD). */
+     * -> 11.35; they replace round 4's ring of camera rays, csg32 3.13 -> 3.07).  Mode
+     * 1's ring of ready paths (12 KB per workgroup) does not fit beside an LDS event
+     * list at 8 workgroups per CU (csg32_nested 10.55 -> 11.76, csg256 balanced 9.30 ->
+     * 10.59 at 4 waves per SIMD), so the event window is in registers (below); mode 2
+     * rings the camera hits (4 KB). */
     bput(&b, "#ifndef WO_CAM_WAVES\n#define WO_CAM_WAVES 1\n#endif\n");
     /* WO_JIT_LDS_EVENTS=0 (WOLOLO_JIT_FLAGS) puts a small tree's event window in
      * registers (wodev::Window) instead of the LDS list */

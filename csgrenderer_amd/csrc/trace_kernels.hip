@@ -340,6 +340,11 @@ constexpr uint32_t kLaneDepthMax = 24;
 #endif
 // dynamic LDS of the BVH walk (stacks + top nodes): with the kernel's static LDS,
 // 8 workgroups of kBlock fit in a CU's 160 KB
+#ifndef WO_LANES_CAM
+#define WO_LANES_CAM 0  // the lane kernels' camera-wave mode (pathtrace_block kCam)
+#endif
+// the camera ring's LDS per workgroup (64 slots of 48 B per wave)
+constexpr size_t kCamRingLds = WO_LANES_CAM ? 4u * 64u * 48u : 0u;
 constexpr size_t kLanesBvhLds = 18u * 1024u;
 
 // component c (a compile-time constant after unrolling) of a float4
@@ -393,6 +398,9 @@ struct LaneTracer {
     static constexpr bool kTerms = kMode == 6 || kMode == 14;
     static constexpr bool kGeneral = kMode == 7;
     static constexpr uint32_t kNodeF4 = kWide ? 7u : 4u;  // float4 per node
+    // camera-ray waves (pathtrace_block): not for the resumable walk, nor for the general
+    // tree (its bits fill the LDS)
+    static constexpr int kCamMode = (kDyn || kGeneral) ? 0 : WO_LANES_CAM;
     WorkCounts wk;
     uint64_t tmark;  // section timing (counting builds)
     const WoRec* __restrict__ prog;      // full program (generic primitives, hit leaves)
@@ -2264,8 +2272,9 @@ static int build_lbvh(WoDev* dev, WoRec const* prog, uint32_t n_recs, uint32_t n
         const size_t stacks =
             ((((size_t)dev->lb_depth * kBlock * (dev->lb_stack16 ? 2u : 4u)) + 15u) & ~(size_t)15u);
         const size_t used = stacks + (dev->lb_general ? (size_t)((gpar.size() + 31u) / 32u) * kBlock * 4u : 0u);
-        const uint32_t top =
-            used < kLanesBvhLds ? (uint32_t)((kLanesBvhLds - used) / (node_f4 * sizeof(float4))) : 0u;
+        // (the kernels with camera-ray waves give the ring's LDS: LaneTracer::kCamMode)
+        const size_t budget = kLanesBvhLds - (dev->lb_wide || dev->lb_general ? 0u : kCamRingLds);
+        const uint32_t top = used < budget ? (uint32_t)((budget - used) / (node_f4 * sizeof(float4))) : 0u;
         dev->lb_top = top < dev->lb_nodes ? top : dev->lb_nodes;
     }
     dev->lb_spheres_only = terms.empty() && !dev->lb_general &&
