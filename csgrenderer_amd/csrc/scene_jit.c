@@ -1735,7 +1735,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "#define WO_LUT lut\n"
          "#endif\n"
          "  __device__ __forceinline__ WoRec hit_leaf(const wodev::Hit& h) const {\n"
-         "    return prog[ordpc[h.ord] + 1u + h.member];\n"
+         "    return prog[ordpc[h.ord()] + 1u + h.member()];\n"
          "  }\n"
          "  __device__ __forceinline__ bool trace(wodev::F3 o, wodev::F3 d, wodev::Hit& hit) {\n");
     if (n_prims == 0) {

@@ -147,7 +147,7 @@ struct InterpTracer {
         return st & 1u;
     }
 
-    __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const { return prog[ordpc[h.ord] + 1u + h.member]; }
+    __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const { return prog[ordpc[h.ord()] + 1u + h.member()]; }
 
     // Nearest change of the root's membership after WO_T_MIN along o + t d.
     __device__ __forceinline__ bool trace(F3 o, F3 d, Hit& hit) {
@@ -443,13 +443,13 @@ struct LaneTracer {
     static constexpr bool kHitMaterial = kSpheresOnly;
     __device__ __forceinline__ WoRec hit_leaf(const Hit& h) const {
         if constexpr (kSpheresOnly)
-            return lleaf[2u * h.ord];  // one load (the record of the ordinal's only member)
+            return lleaf[2u * h.ord()];  // one load (the record of the ordinal's only member)
         else
-            return prog[ordpc[h.ord] + 1u + h.member];
+            return prog[ordpc[h.ord()] + 1u + h.member()];
     }
     // the leaf's material, copied next to its record: loaded beside it, not after it
     __device__ __forceinline__ WoMaterial hit_material(const Hit& h, const WoMaterial* __restrict__) const {
-        return reinterpret_cast<const WoMaterial*>(lleaf)[2u * h.ord + 1u];
+        return reinterpret_cast<const WoMaterial*>(lleaf)[2u * h.ord() + 1u];
     }
 
     // Interval of primitive `ord` (the interpreter's arithmetic, bit for bit).

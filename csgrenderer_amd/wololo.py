@@ -30,7 +30,7 @@ WO_T_MIN = 1.0e-3
 # wo_scene.h WO_WORK_* (executed-work counters)
 WORK_KINDS = ("segments", "sphere_tests", "halfspace_tests", "bound_tests", "events", "sweep_steps", "recollects",
               "primary_segments", "cyc_take", "cyc_collect", "cyc_sweep", "cyc_shade", "cyc_loop", "idle_lanes",
-              "sweep_trips")
+              "sweep_trips", "cyc_cam")
 WO_NODE_INVALID = 0xFFFFFFFF
 
 

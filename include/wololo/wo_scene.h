@@ -139,7 +139,8 @@ enum {
     /* lane occupancy (counting launches): */
     WO_WORK_IDLE_LANES = 13,     /* loop iterations of a lane with no path (queue drained) */
     WO_WORK_SWEEP_TRIPS = 14,    /* sweep loop trips of a wave (64 lane slots each) */
-    WO_WORK_KINDS = 15
+    WO_WORK_CYC_CAM = 15,        /* wave cycles of camera-ray iterations (WO_TIME_SECTIONS) */
+    WO_WORK_KINDS = 16
 };
 
 /* Minimum ray parameter for every CSG segment (RTIOW's 0.001). */
