@@ -1909,14 +1909,17 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         }
     }
 kernel_tail:
-    /* Waves per SIMD the register budget is sized for (measured, 1920x1080x64):
+    /* Waves per SIMD the register budget is sized for (measured, 1920x1080x64; round
+     * 5, with camera-ray waves: the union count 9.39 / 9.24 / 9.55 ms at 8 / 7 / 6 -- at 8
+     * it spills 35 VGPRs, 9.6 GB of scratch writes per frame -- csg32_nested 8.83 / 8.92
+     * at 8 / 7, chain 11.47 / 11.81):
      * csg256 balanced / chain (128 primitives) 23.7 / 38.0 ms at 6, 21.3 / 33.8 at
      * 8; csg32 (18) 5.24 ms at 7 (8 LDS events), 5.19 at 8 (7 LDS events: 8
      * workgroups' LDS fit the CU only then). */
     bput(&b,
          "\n#ifndef WO_JIT_MIN_WAVES\n"
          "#define WO_JIT_MIN_WAVES %u\n#endif\n",
-         (n_prims > 64u || g.lds_events) ? 8u : 7u);
+         n_uterms ? 7u : (n_prims > 64u || g.lds_events) ? 8u : 7u);
     bput(&b,
          "extern \"C\" __global__ __launch_bounds__(256, WO_JIT_MIN_WAVES) void wo_jit_pathtrace(\n"
          "    const WoRec* __restrict__ prog, const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t local_rows,\n"

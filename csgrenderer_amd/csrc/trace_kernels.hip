@@ -2758,9 +2758,12 @@ static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, u
         // (tools/root_step.py, N = 8 projection): 3 tiles per resident workgroup instead
         // of 8 (8x4 at N = 8): csg32 6.37 -> 6.62x, csg256 balanced 6.79 -> 4.18x,
         // chain 6.83 -> 4.75x, csg32_nested 6.35 -> 5.83x, RTIOW 6.59 -> 6.63x; kept at 8.
-        const uint64_t want_tiles = 8ull * resident;
+        const char* tw = getenv("WOLOLO_TILE_WANT");  // (measurement) tiles per resident workgroup
+        const char* ts = getenv("WOLOLO_TILE_SPAN");  // (measurement) 8x8 tiles may span two row bands
+        const uint64_t want_tiles = (uint64_t)(tw && *tw ? atoi(tw) : 8) * resident;
+        const bool span = ts && *ts == '1';
         big = 3u | (3u << 4);
-        if ((uint64_t)tiles_across(width, big) * (rows >> 3) < want_tiles || band_rows < 8u) {
+        if ((uint64_t)tiles_across(width, big) * (rows >> 3) < want_tiles || (band_rows < 8u && !span)) {
             big = 3u | (2u << 4);
             tail_rounds = 2.0;
         }
