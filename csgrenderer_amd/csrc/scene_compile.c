@@ -22,6 +22,7 @@
  *   5. subtrees with >= 2 leaves and a finite extent get a conservative
  *      WO_OP_BOUND sphere so a wave whose rays all miss can skip them.
  */
+#include <float.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -676,6 +677,14 @@ static void emit_leaf(Ctx* c, const ENode* m) {
     if (!rec) return;
     rec->u0 = m->material;
     if (m->kind == E_SPHERE) {
+        /* every fp32 value of the record finite: the kernels' square root of the
+         * discriminant r^2 - ll (sqrt_cr) is exact below +inf only */
+        const double r2 = m->rad * m->rad;
+        if (!(r2 < (double)FLT_MAX) || !isfinite(m->c[0]) || !isfinite(m->c[1]) || !isfinite(m->c[2]) ||
+            !(fabs(m->c[0]) < (double)FLT_MAX && fabs(m->c[1]) < (double)FLT_MAX && fabs(m->c[2]) < (double)FLT_MAX)) {
+            fail(c, "sphere leaf out of fp32 range (radius^2 or centre not finite)");
+            return;
+        }
         rec->op = WO_LEAF_SPHERE;
         rec->f[0] = (float)m->c[0];
         rec->f[1] = (float)m->c[1];

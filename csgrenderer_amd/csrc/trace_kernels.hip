@@ -1437,6 +1437,7 @@ struct WoDev {
     // scene-specialised kernel (hiprtc)
     hipModule_t jit_module;
     hipFunction_t jit_fn;
+    uint32_t jit_share_tiles;  // big tiles per resident workgroup for the specialised kernel (plan_tiles)
     std::string jit_key;  // SHA-256 (hex) of the loaded code object's inputs
     std::string jit_src;  // its source (the counting variant is built from it on demand)
     hipModule_t count_module;
@@ -2620,6 +2621,11 @@ extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t err
     dev->jit_fn = fn;
     dev->jit_key = key;
     dev->jit_src = src;
+    {
+        const char* m = strstr(src, "// wo_share_tiles ");
+        const int v = m ? atoi(m + strlen("// wo_share_tiles ")) : 0;
+        dev->jit_share_tiles = v >= 1 && v <= 64 ? (uint32_t)v : 8u;
+    }
     dev->jit_origin = origin;
     dev->jit_compile_sec = sec;
     return 0;
@@ -2732,7 +2738,8 @@ static uint32_t shape_of(const char* f) {
 }
 static uint32_t tiles_across(uint32_t width, uint32_t shape) { return (width + (1u << (shape & 15u)) - 1u) >> (shape & 15u); }
 
-static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, uint32_t band_rows) {
+static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, uint32_t band_rows,
+                             uint32_t want_per_wg) {
     const uint32_t s44 = 2u | (2u << 4);
     PathLaunch g = {};
     // the tail's tiles: 4x4 (2x2 / 4x2 for an 8-rank share's tail: within noise,
@@ -2758,9 +2765,17 @@ static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, u
         // (tools/root_step.py, N = 8 projection): 3 tiles per resident workgroup instead
         // of 8 (8x4 at N = 8): csg32 6.37 -> 6.62x, csg256 balanced 6.79 -> 4.18x,
         // chain 6.83 -> 4.75x, csg32_nested 6.35 -> 5.83x, RTIOW 6.59 -> 6.63x; kept at 8.
+        // Round 5 (camera-ray waves, tools/root_step.py at N = 8 without the present
+        // map-back, band 5:1): small tiles now cost more -- a wave drains its last paths
+        // at the end of every tile, and a 4x4 tile gives a wave 4 camera iterations (the
+        // whole csg32 frame in 4x4 tiles: 2.77 -> 3.33 ms) -- so the specialised kernels
+        // of trees up to depth 32 (the generator's `wo_share_tiles`) want 3 tiles per
+        // resident workgroup: csg32 6.30 -> 6.87x, csg32_nested 7.09 -> 7.66x, csg256
+        // balanced 6.88 -> 7.19x; the chain keeps 8 (6.96 -> 6.46x with 3: its costly tiles
+        // set the end of a share); the lane tracer keeps 8.
         const char* tw = getenv("WOLOLO_TILE_WANT");  // (measurement) tiles per resident workgroup
         const char* ts = getenv("WOLOLO_TILE_SPAN");  // (measurement) 8x8 tiles may span two row bands
-        const uint64_t want_tiles = (uint64_t)(tw && *tw ? atoi(tw) : 8) * resident;
+        const uint64_t want_tiles = (uint64_t)(tw && *tw ? (uint32_t)atoi(tw) : want_per_wg) * resident;
         const bool span = ts && *ts == '1';
         big = 3u | (3u << 4);
         if ((uint64_t)tiles_across(width, big) * (rows >> 3) < want_tiles || (band_rows < 8u && !span)) {
@@ -2961,7 +2976,7 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
         // a rank's local rows are bands of tile_rows consecutive frame rows: a tile
         // taller than a band would join rows far apart (incoherent primary rays)
         PathLaunch tg = plan_tiles(fr.width, local_rows, (uint32_t)dev->cus * (uint32_t)per_cu,
-                                   fr.nranks > 1u ? fr.tile_rows : ~0u);
+                                   fr.nranks > 1u ? fr.tile_rows : ~0u, kind == kJit ? dev->jit_share_tiles : 8u);
         if (d_accum && fr.mode == WO_MODE_PATHTRACE) {
             tg.acc = d_accum;
             tg.acc_spp = accum_spp;

@@ -567,9 +567,12 @@ def default_band(nranks: int):
     receives the gather, assembles and presents) sits out one round of bands in
     every `cycle`.  tools/root_step.py, csg32 1080p64, N = 8: 0:0 6.21x, 8:1 6.37x,
     12:1 6.44x; N = 4: 0:0 3.33x, 16:1 3.59x; N = 2: 0:0 1.89x, 32:1 1.92x.  Heavier
-    scenes want a lighter skip (rank 0's extra work is the same milliseconds)."""
+    scenes want a lighter skip (rank 0's extra work is the same milliseconds).  Round 5
+    (camera-ray waves make the shares shorter, rank 0's extra work is not): N = 8 without
+    the present map-back, csg32 10:1 6.69x / 5:1 6.87x, csg32_nested 7.29 / 7.66x, RTIOW
+    7.45 / 7.36x (profiles/r05_root_step_nomap_n8.log)."""
     if nranks >= 8:
-        return (10, 1)
+        return (5, 1)
     if nranks >= 4:
         return (16, 1)
     if nranks >= 2:

@@ -261,3 +261,21 @@ def test_deep_difference_chain_fails_cleanly(hostonly):
             with pytest.raises(wl.WololoError, match="too deep"):
                 r.compile()
         r.close()
+
+
+def test_sphere_leaf_out_of_fp32_range_fails_cleanly(hostonly):
+    """A sphere whose radius^2 or centre is not a finite fp32 value is refused by the
+    compiler: the kernels' square root of the discriminant (sqrt_cr, rsq + one Markstein
+    step) is exact for every finite argument but gives NaN at +inf, and a
+    finite r^2 with a finite ray keeps the discriminant below +inf.  1e19 (r^2 = 1e38)
+    still compiles."""
+    for rad, off, ok in [(1e19, 0.0, True), (2e19, 0.0, False), (1.0, 1e39, False)]:
+        r = wl.Renderer("big", max_nodes=8)
+        s, t = r.sphere(rad), r.sphere(1.0)
+        r.union(wl.arg(s, (off, 0.0, 0.0)), wl.arg(t))
+        if ok:
+            assert r.compile() > 0
+        else:
+            with pytest.raises(wl.WololoError, match="fp32 range"):
+                r.compile()
+        r.close()

@@ -3,7 +3,7 @@
 # (kernel stats, HBM bytes, instruction mix) for every kernel the bench runs, and
 # rank 0's N-GPU step with the present map-back for every config.  Results under
 # gpurun_out/; tools/pmc_summary.py turns the profiles into profiles/ summaries.
-#   tools/evidence_r05.sh bench|prof1|prof2|rs
+#   tools/evidence_r05.sh bench|prof1|prof2|rs|rsnomap
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 S=tools/gpu_session.sh
@@ -42,5 +42,11 @@ rs)
         "rsrt:300:python tools/root_step.py --scene rtiow_cover --worlds 2 4 8 --map-back bgra > gpurun_out/r05_root_step_rtiow.log 2>&1" \
         "rs512:300:python tools/root_step.py --scene csg512_balanced --worlds 2 4 8 --map-back bgra > gpurun_out/r05_root_step_512b.log 2>&1" \
         "rsc4:400:python tools/root_step.py --scene csg32 --width 3840 --height 2160 --spp 256 --worlds 2 4 8 --map-back bgra > gpurun_out/r05_root_step_c4.log 2>&1"
+    ;;
+rsnomap)
+    # the same without the present map-back (bench.py's N-GPU frame is not presented)
+    for sc in csg32 csg32_nested csg256_balanced csg256_chain rtiow_cover csg512_balanced; do
+        bash $S "nm_$sc:300:python tools/root_step.py --scene $sc --worlds 2 4 8 --map-back none > gpurun_out/r05_root_step_nomap_$sc.log 2>&1" || exit $?
+    done
     ;;
 esac
