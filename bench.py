@@ -71,6 +71,11 @@ def parse():
     ap.add_argument("--jit", type=int, default=None, help="legacy: 0 = --tracer interpreter")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo stages the gather through host memory (for rehearsing N>1 ranks on one GPU)")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="N>1: GPU_MAX_HW_QUEUES for this rank's process (HIP's default is 4; rank 0's two "
+                         "render streams, its gather stream and the default stream then share queues, and a "
+                         "render queued behind a gather stops overlapping the previous frame; 0 = leave the "
+                         "environment alone)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N>1: gather each frame before the next renders (default: frame k+1 renders while frame k "
                          "is gathered, with either backend)")
@@ -136,6 +141,10 @@ def main():
     world = int(world_env or "1")
     if world != args.gpus:
         fail(f"--gpus {args.gpus} but {world} ranks are running (WORLD_SIZE)")
+    if world > 1 and args.hw_queues > 0:
+        # before the first HIP call of this process (tools/root_step.py, N = 8, rank 0's
+        # step: csg32 0.385 -> 0.355 ms, csg32_nested 1.116 -> 0.945 ms with 8 queues)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 16))
     import torch
     import torch.distributed as dist
 
@@ -196,11 +205,17 @@ def main():
         stacked = torch.empty((world, lr, W, 4), dtype=torch.float32, device="cpu" if gloo else dev)
         gathered = list(stacked.unbind(0))
         frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
-    cs = torch.cuda.current_stream(dev)  # gather + assemble (RCCL's stream follows it)
-    # render streams (one per buffer when frames overlap)
-    if args.frames_in_flight > 1:
-        rss = [torch.cuda.Stream(dev) for _ in range(nbuf)]
-    else:
+    # render streams (one per buffer when frames overlap), then the gather + assemble
+    # stream (RCCL's stream follows the current one).  N > 1: a created stream made
+    # current, not the default stream: kernels on the default stream leave the two
+    # render streams sharing a hardware queue (the box has 4), so frame k+1 no longer
+    # overlaps frame k's tail (tools/root_step.py --streams null vs bench, N = 8:
+    # csg32 share 0.437 vs 0.399 ms, csg256 chain 1.77 vs 1.66 ms)
+    rss = [torch.cuda.Stream(dev) for _ in range(nbuf)] if args.frames_in_flight > 1 else None
+    if world > 1:
+        torch.cuda.set_stream(torch.cuda.Stream(dev))
+    cs = torch.cuda.current_stream(dev)
+    if rss is None:
         rss = [torch.cuda.Stream(dev) if pipelined else cs] * nbuf
     k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     k_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -315,7 +330,8 @@ def main():
                            {"parallelism": parallelism, "ranks": world, "devices": min(world, ndev),
                             "launcher": "torchrun" if world_env else "none",
                             "frames_in_flight": args.frames_in_flight, "prewarm_frames": prewarm,
-                            **({"row_bands": f"{args.band_w[0]}:{args.band_w[1]}"} if world > 1 else {})})
+                            **({"row_bands": f"{args.band_w[0]}:{args.band_w[1]}",
+                                "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default")} if world > 1 else {})})
         if verified is not None:
             line["verified_vs_full_render"] = verified
         if world == 1 and info.mode == wl.MODE_PATHTRACE and not args.no_draw_frame:

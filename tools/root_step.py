@@ -53,9 +53,19 @@ def main():
     ap.add_argument("--band", default="auto",
                     help="row-band weighting CYCLE:SKIP (rank 0 sits out SKIP of every CYCLE rounds), 'auto' = "
                          "wololo.default_band(N) as bench.py uses it, '0:0' = a band per rank and round")
+    ap.add_argument("--streams", default="bench", choices=["bench", "null", "split"],
+                    help="rank 0's streams: 'bench' = bench.py's two render streams + one created stream "
+                         "for the copies, assemble, encode and D2H; 'null' = the same on the default stream "
+                         "(bench.py before round 5: its kernels leave the two render streams on one hardware "
+                         "queue, so consecutive frames stop overlapping); 'split' = separate copy / assemble / "
+                         "D2H streams (rounds 3-5)")
     ap.add_argument("--map-back", default="bgra", choices=["bgra", "float", "none"],
                     help="rank 0's D2H of the presented frame after the encode (draw_frame: bgra)")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process, as bench.py sets it at N > 1 (0: leave it)")
     args = ap.parse_args()
+    if args.hw_queues > 0:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 16))
 
     import torch
     from csgrenderer_amd import scenes
@@ -105,7 +115,12 @@ def main():
         lr = wl.local_rows(H, T, n, band)
         share_bytes = lr * W * 16
         rs = [torch.cuda.Stream(), torch.cuda.Stream()]
-        cps, asm, d2h = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+        if args.streams == "null":
+            cps = asm = d2h = main_s
+        elif args.streams == "bench":
+            cps = asm = d2h = torch.cuda.Stream()
+        else:
+            cps, asm, d2h = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
         gather = [torch.empty((n, lr, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
         frames = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
         bgra = [torch.empty((H, W), dtype=torch.int32, device="cuda") for _ in range(2)]
