@@ -1960,8 +1960,9 @@ kernel_tail:
      * executed-work roofline (0: not known, e.g. the postfix form) */
     if (eval_ops) bput(&b, "// wo_eval_ops_per_event %u\n", eval_ops);
     /* big tiles per resident workgroup the launch plan wants (trace_kernels.hip plan_tiles):
-     * 3 for trees up to depth 32, 8 for deep ones (the chain's costly tiles) */
-    bput(&b, "// wo_share_tiles %u\n", g.lds_events ? 3u : 8u);
+     * 3 for every tree since bench.py's renders stopped sharing a hardware queue (the
+     * chain kept 8 before: 6.88 -> 6.99x at N = 8 with 3 now) */
+    bput(&b, "// wo_share_tiles %u\n", 3u);
     free(g.dls);
     free(lut.table);
     free(uterms);

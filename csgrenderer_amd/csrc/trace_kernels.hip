@@ -345,7 +345,11 @@ constexpr uint32_t kLaneDepthMax = 24;
 #endif
 // the camera ring's LDS per workgroup (64 slots of 48 B per wave)
 constexpr size_t kCamRingLds = WO_LANES_CAM ? 4u * 64u * 48u : 0u;
-constexpr size_t kLanesBvhLds = 18u * 1024u;
+// 8 workgroups per CU = 20 KB each, less the kernels' static LDS (2224 B since the
+// pixel-row table, round 5; at 18 KB of dynamic LDS the total crossed 20 KB and the
+// RTIOW cover ran at 7 workgroups per CU: 11.24 -> 11.69 ms)
+constexpr size_t kLanesStaticLdsMax = 2304u;
+constexpr size_t kLanesBvhLds = 20u * 1024u - kLanesStaticLdsMax;
 
 // component c (a compile-time constant after unrolling) of a float4
 __device__ __forceinline__ float f4c(const float4& v, int c) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); }
@@ -401,6 +405,7 @@ struct LaneTracer {
     // camera-ray waves (pathtrace_block): not for the resumable walk, nor for the general
     // tree (its bits fill the LDS)
     static constexpr int kCamMode = (kDyn || kGeneral) ? 0 : WO_LANES_CAM;
+    static constexpr bool kFreshTail = kDyn || kGeneral;  // (TracerFreshTail)
     WorkCounts wk;
     uint64_t tmark;  // section timing (counting builds)
     const WoRec* __restrict__ prog;      // full program (generic primitives, hit leaves)
@@ -2772,7 +2777,12 @@ static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, u
         // of trees up to depth 32 (the generator's `wo_share_tiles`) want 3 tiles per
         // resident workgroup: csg32 6.30 -> 6.87x, csg32_nested 7.09 -> 7.66x, csg256
         // balanced 6.88 -> 7.19x; the chain keeps 8 (6.96 -> 6.46x with 3: its costly tiles
-        // set the end of a share); the lane tracer keeps 8.
+        // set the end of a share); the lane tracer keeps 8.  Those runs put rank 0's five
+        // streams on HIP's 4 hardware queues, so a render could queue behind a copy; with
+        // bench.py's layout (two render streams + one gather stream, 8 queues) 3 wins for
+        // every scene (want 3 / 8, N = 8 projection): csg32 6.86 / 6.40x, csg32_nested
+        // 7.67 / 7.27x, balanced 7.17 / 6.78x, chain 6.99 / 6.88x, RTIOW 7.37 / 6.97x,
+        // csg512 6.00 / 5.45x, C4 7.59 / 7.60x (profiles/r05_root_step_want_hwq8.log).
         const char* tw = getenv("WOLOLO_TILE_WANT");  // (measurement) tiles per resident workgroup
         const char* ts = getenv("WOLOLO_TILE_SPAN");  // (measurement) 8x8 tiles may span two row bands
         const uint64_t want_tiles = (uint64_t)(tw && *tw ? (uint32_t)atoi(tw) : want_per_wg) * resident;
@@ -2976,7 +2986,7 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
         // a rank's local rows are bands of tile_rows consecutive frame rows: a tile
         // taller than a band would join rows far apart (incoherent primary rays)
         PathLaunch tg = plan_tiles(fr.width, local_rows, (uint32_t)dev->cus * (uint32_t)per_cu,
-                                   fr.nranks > 1u ? fr.tile_rows : ~0u, kind == kJit ? dev->jit_share_tiles : 8u);
+                                   fr.nranks > 1u ? fr.tile_rows : ~0u, kind == kJit ? dev->jit_share_tiles : 3u);
         if (d_accum && fr.mode == WO_MODE_PATHTRACE) {
             tg.acc = d_accum;
             tg.acc_spp = accum_spp;
