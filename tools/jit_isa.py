@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--keep", default=None, help="copy the .s here")
     ap.add_argument("--src", default=None, help="compile this (edited) generated source instead of the scene's")
     ap.add_argument("--dump", default=None, help="write the scene's generated source here")
+    ap.add_argument("--rtc", action="store_true",
+                    help="compile through hiprtc with the runtime's options (trace_kernels.hip jit_options) "
+                         "and read the code object's resource notes, instead of hipcc -S")
     a = ap.parse_args()
     from csgrenderer_amd import scenes
     from csgrenderer_amd import wololo as wl
@@ -34,6 +37,8 @@ def main():
     src = open(a.src).read() if a.src else r.jit_source()
     if a.dump:
         open(a.dump, "w").write(src)
+    if a.rtc:
+        return rtc(src, a.D, a.keep)
     d = tempfile.mkdtemp()
     os.makedirs(os.path.join(d, "wololo"))
     shutil.copy(os.path.join(ROOT, "csgrenderer_amd/csrc/wo_device_common.h"), d)
@@ -61,6 +66,54 @@ def main():
             print(f"  {k:28s}{v}")
     if a.keep:
         shutil.copy(os.path.join(d, "k.s"), a.keep)
+    shutil.rmtree(d)
+    return 0
+
+
+def rtc(src, defs, keep):
+    """hiprtc compile as jit_compile does (same embedded headers and options)."""
+    import ctypes
+    lib = ctypes.CDLL("/opt/rocm/lib/libhiprtc.so")
+    hdrs = [open(os.path.join(ROOT, "csgrenderer_amd/csrc/wo_device_common.h"), "rb").read(),
+            open(os.path.join(ROOT, "include/wololo/wo_scene.h"), "rb").read()]
+    names = [b"wo_device_common.h", b"wololo/wo_scene.h"]
+    prog = ctypes.c_void_p()
+    H = ctypes.c_char_p * 2
+    rc = lib.hiprtcCreateProgram(ctypes.byref(prog), src.encode(), b"wo_scene_jit.hip", 2, H(*hdrs), H(*names))
+    if rc:
+        print("hiprtcCreateProgram", rc)
+        return 1
+    opts = [b"--offload-arch=gfx950", b"-O3", b"-ffp-contract=off", b"-std=c++17", b"-fno-slp-vectorize"]
+    opts += [f"-D{x}".encode() for x in defs]
+    extra = os.environ.get("WOLOLO_JIT_FLAGS", "")
+    opts += [x.encode() for x in extra.split()]
+    O = ctypes.c_char_p * len(opts)
+    rc = lib.hiprtcCompileProgram(prog, len(opts), O(*opts))
+    if rc:
+        n = ctypes.c_size_t()
+        lib.hiprtcGetProgramLogSize(prog, ctypes.byref(n))
+        log = ctypes.create_string_buffer(n.value + 1)
+        lib.hiprtcGetProgramLog(prog, log)
+        print(log.value.decode()[-3000:])
+        return 1
+    n = ctypes.c_size_t()
+    lib.hiprtcGetCodeSize(prog, ctypes.byref(n))
+    code = ctypes.create_string_buffer(n.value)
+    lib.hiprtcGetCode(prog, code)
+    d = tempfile.mkdtemp()
+    co = os.path.join(d, "k.co")
+    open(co, "wb").write(code.raw)
+    notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co], capture_output=True, text=True).stdout
+    for key in (".name:", ".vgpr_count", ".sgpr_count", ".vgpr_spill_count", ".sgpr_spill_count",
+                ".private_segment_fixed_size", ".group_segment_fixed_size"):
+        for line in notes.splitlines():
+            if line.strip().startswith(key):
+                print(line.strip())
+    dis = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "-d", "--mcpu=gfx950", co], capture_output=True,
+                         text=True).stdout
+    print("scratch stores:", dis.count("scratch_store"), "loads:", dis.count("scratch_load"))
+    if keep:
+        open(keep, "w").write(dis)
     shutil.rmtree(d)
     return 0
 
