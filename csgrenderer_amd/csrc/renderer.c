@@ -527,6 +527,10 @@ static void jit_job_poll(Wo_Renderer* r, int wait) {
         if (!ok)
             for (uint32_t i = 0; i < r->ndevs; ++i) (void)wo_dev_set_jit(r->devs[i], NULL, err, sizeof err);
         r->jit_loaded = ok;
+        if (ok && r->lanes_loaded) { /* the lanes ran while it compiled (sync_device_ex) */
+            for (uint32_t i = 0; i < r->ndevs; ++i) wo_dev_set_lanes(r->devs[i], 0);
+            r->lanes_loaded = 0;
+        }
         if (cur >= 0) (void)wo_dev_select(cur);
     }
     free(src);
@@ -588,18 +592,42 @@ static int sync_device_ex(Wo_Renderer* r, int may_defer) {
         int want_lanes = lanes_ok && (r->tracer == WO_TRACER_LANES ||
                                       (r->tracer == WO_TRACER_AUTO && r->n_prims > lanes_min) ||
                                       (r->tracer == WO_TRACER_JIT && r->n_prims > max_prims));
-        int want_jit = !want_lanes && r->tracer != WO_TRACER_INTERPRETER && r->n_prims > 0 && r->n_prims <= max_prims;
+        /* A general tree above max_prims whose root the levelled truth tables
+         * evaluate (scene_jit.c hlut_plan; not a union of terms or of primitives,
+         * which the lane tracer's union count and term mode take): the specialised
+         * kernel, with the lanes only while it compiles in the background
+         * (csg360_nested 201.6 ms against the lanes' general walk, 324.4).
+         * WOLOLO_JIT_GENERAL=0 keeps such scenes on the lanes. */
+        char* pre_src = NULL;
+        const char* jg = getenv("WOLOLO_JIT_GENERAL");
+        if (r->tracer != WO_TRACER_INTERPRETER && r->tracer != WO_TRACER_LANES && r->n_prims > max_prims &&
+            r->n_prims <= 1023u && !(jg && strcmp(jg, "0") == 0)) {
+            pre_src = wo_generate_jit_source(r->prog, r->n_recs, r->n_prims);
+            if (pre_src && !strstr(pre_src, "#define WO_JIT_HLUT 1\n")) {
+                free(pre_src);
+                pre_src = NULL;
+            }
+        }
+        const int lanes_meanwhile = pre_src != NULL && want_lanes;
+        if (pre_src) want_lanes = 0;
+        int want_jit = !want_lanes && r->tracer != WO_TRACER_INTERPRETER && r->n_prims > 0 &&
+                       (r->n_prims <= max_prims || pre_src != NULL);
         for (uint32_t i = 0; i < r->ndevs; ++i) wo_dev_set_lanes(r->devs[i], want_lanes);
         r->lanes_loaded = want_lanes;
         int deferred = 0;
         if (want_jit) {
-            char* src = wo_generate_jit_source(r->prog, r->n_recs, r->n_prims);
+            char* src = pre_src ? pre_src : wo_generate_jit_source(r->prog, r->n_recs, r->n_prims);
+            pre_src = NULL;
             if (!src) {
                 fprintf(stderr, WO_LOG_PREFIX " scene specialisation: source generation failed; using the interpreter\n");
             } else if (may_defer && !wo_dev_jit_cached(r->dev, src) && (r->jit_job = wo_jit_job_start(r->dev, src))) {
-                r->jit_want = src; /* compiling in the background; the interpreter meanwhile */
+                r->jit_want = src; /* compiling in the background; the interpreter (or the lanes) meanwhile */
                 src = NULL;
                 deferred = 1;
+                if (lanes_meanwhile) { /* a loaded specialised kernel takes precedence (wo_dev_launch_ex) */
+                    for (uint32_t i = 0; i < r->ndevs; ++i) wo_dev_set_lanes(r->devs[i], 1);
+                    r->lanes_loaded = 1;
+                }
             } else {
                 /* compiled once (code-object cache), loaded on every rank's device */
                 int ok = 1;

@@ -1445,6 +1445,232 @@ static void lut_emit_eval(Buf* b, const LutPlan* pl, int indent) {
     bput(b, "%*sr = (0x%08xu >> lsub) & 1u;  // the root from the %u subtree values\n", indent, "", pl->top, pl->k);
 }
 
+/* ---- root evaluation by levels of truth tables (larger general trees) ----
+ * A general tree too big for lut_plan (csg360_nested: 309 primitives under 308
+ * unions, intersections and differences) is cut in levels: level 1's units are
+ * the maximal subtrees of <= HLUT_MAX_BITS primitives, level l + 1's the maximal
+ * subtrees of <= HLUT_MAX_BITS level-l units, up to the root, a unit of its own.
+ * A unit's value is one bit of its truth table indexed by its lower units'
+ * values (a contiguous range of them: they are numbered left to right), so an
+ * event updates one unit per level -- its primitive's, then that unit's parent
+ * unit, ... -- instead of re-evaluating the tree: per level one LDS read of the
+ * lower index's entry (its unit, the unit's range and table offset) and one of
+ * the table.  The same event order and values as the flat evaluation, so the
+ * hit is the same key bit for bit. */
+#define HLUT_MAX_BITS 8u
+#define HLUT_MAX_LEVELS 4u
+#define HLUT_MAX_WORDS 1024u /* table words: 10-bit offsets in an entry */
+typedef struct HPlan {
+    uint32_t L;                       /* levels; level L has one unit, the root */
+    uint32_t k[HLUT_MAX_LEVELS];      /* units per level */
+    uint32_t base[HLUT_MAX_LEVELS];   /* level's first entry in info[] (one per lower index) */
+    uint32_t ubase[HLUT_MAX_LEVELS];  /* level's first unit in ulo / un / uoff */
+    uint32_t *info, ninfo;            /* unit | lo << 8 | n << 18 | off << 22 */
+    uint32_t *ulo, *un, *uoff, nunits;
+    uint32_t *table, words;
+} HPlan;
+
+static void hplan_free(HPlan* h) {
+    free(h->info);
+    free(h->ulo);
+    free(h->un);
+    free(h->uoff);
+    free(h->table);
+    memset(h, 0, sizeof *h);
+}
+
+/* units below x at the current level (unit_of[y] >= 0: y roots lower unit unit_of[y]) */
+static uint32_t h_count(const TNode* t, int x, const int* unit_of, uint32_t* cnt, uint32_t* first) {
+    if (unit_of[x] >= 0) {
+        cnt[x] = 1u;
+        first[x] = (uint32_t)unit_of[x];
+        return 1u;
+    }
+    const uint32_t a = h_count(t, t[x].l, unit_of, cnt, first), b = h_count(t, t[x].r, unit_of, cnt, first);
+    cnt[x] = a + b;
+    first[x] = first[t[x].l] < first[t[x].r] ? first[t[x].l] : first[t[x].r];
+    return a + b;
+}
+
+static int h_eval(const TNode* t, int x, const int* unit_of, uint32_t lo, uint32_t idx) {
+    if (unit_of[x] >= 0) return (int)((idx >> ((uint32_t)unit_of[x] - lo)) & 1u);
+    const TNode* n = &t[x];
+    const int a = h_eval(t, n->l, unit_of, lo, idx), b = h_eval(t, n->r, unit_of, lo, idx);
+    return n->op == WO_OP_UNION ? (a | b) : n->op == WO_OP_INTER ? (a & b) : n->op == WO_OP_DIFF ? (a & !b) : (b & !a);
+}
+
+/* the maximal subtrees of <= HLUT_MAX_BITS units, in lower-index order */
+static void h_split(const TNode* t, int x, const uint32_t* cnt, const uint32_t* first, int* roots, uint32_t* nr) {
+    if (cnt[x] <= HLUT_MAX_BITS) {
+        roots[(*nr)++] = x;
+        return;
+    }
+    const int a = t[x].l, b = t[x].r;
+    const int lo_first = first[a] <= first[b];
+    h_split(t, lo_first ? a : b, cnt, first, roots, nr);
+    h_split(t, lo_first ? b : a, cnt, first, roots, nr);
+}
+
+static int hlut_plan(const WoRec* prog, uint32_t n_recs, uint32_t n_prims, HPlan* h) {
+    memset(h, 0, sizeof *h);
+    if (n_prims < 2u || n_prims > 1023u) return 0;
+    const uint32_t cap = 2u * n_prims;
+    TNode* t = (TNode*)malloc(sizeof(TNode) * cap);
+    int* st = (int*)malloc(sizeof(int) * (n_prims + 1u));
+    int* unit_of = (int*)malloc(sizeof(int) * cap);
+    int* roots = (int*)malloc(sizeof(int) * cap);
+    uint32_t* cnt = (uint32_t*)malloc(sizeof(uint32_t) * cap);
+    uint32_t* first = (uint32_t*)malloc(sizeof(uint32_t) * cap);
+    h->info = (uint32_t*)malloc(sizeof(uint32_t) * (n_prims + HLUT_MAX_LEVELS * 256u));
+    /* (at most 255 units per level) */
+    h->ulo = (uint32_t*)malloc(sizeof(uint32_t) * HLUT_MAX_LEVELS * 256u);
+    h->un = (uint32_t*)malloc(sizeof(uint32_t) * HLUT_MAX_LEVELS * 256u);
+    h->uoff = (uint32_t*)malloc(sizeof(uint32_t) * HLUT_MAX_LEVELS * 256u);
+    h->table = (uint32_t*)calloc(HLUT_MAX_WORDS, sizeof(uint32_t));
+    int ok = t && st && unit_of && roots && cnt && first && h->info && h->ulo && h->un && h->uoff && h->table;
+    uint32_t nt = 0, sp = 0;
+    for (uint32_t pc = 0; pc < n_recs && ok;) {
+        const WoRec* r = &prog[pc];
+        if (r->op == WO_OP_PRIM) {
+            ok = nt < cap && sp <= n_prims && r->u1 < n_prims;
+            if (!ok) break;
+            TNode x = {0, -1, -1, r->u1, 1u};
+            t[nt] = x;
+            st[sp++] = (int)nt++;
+            pc += 1u + r->u0;
+            continue;
+        }
+        ++pc;
+        if (r->op == WO_OP_BOUND) continue;
+        ok = sp >= 2u && nt < cap;
+        if (!ok) break;
+        const int b = st[--sp], a = st[--sp];
+        TNode x = {(int)r->op, a, b, t[a].lo < t[b].lo ? t[a].lo : t[b].lo, t[a].n + t[b].n};
+        t[nt] = x;
+        st[sp++] = (int)nt++;
+    }
+    ok = ok && sp == 1u && t[st[0]].n == n_prims;
+    const int root = ok ? st[0] : 0;
+    /* level 0's units: the primitives (their ordinals) */
+    for (uint32_t x = 0; ok && x < nt; ++x) unit_of[x] = t[x].op == 0 ? (int)t[x].lo : -1;
+    uint32_t nlow = n_prims;
+    while (ok) {
+        if (h->L == HLUT_MAX_LEVELS) {
+            ok = 0;
+            break;
+        }
+        const uint32_t L = h->L;
+        h_count(t, root, unit_of, cnt, first);
+        uint32_t k = 0;
+        h_split(t, root, cnt, first, roots, &k);
+        ok = k >= 1u && k <= 255u;
+        h->k[L] = k;
+        h->base[L] = h->ninfo;
+        h->ubase[L] = h->nunits;
+        for (uint32_t j = 0; ok && j < k; ++j) {
+            const int x = roots[j];
+            const uint32_t lo = first[x], n = cnt[x];
+            const uint32_t w = n >= 5u ? 1u << (n - 5u) : 1u;
+            ok = lo < 1024u && h->words + w <= HLUT_MAX_WORDS && lo + n <= nlow;
+            if (!ok) break;
+            const uint32_t off = h->words;
+            h->words += w;
+            for (uint32_t idx = 0; idx < (1u << n); ++idx)
+                if (h_eval(t, x, unit_of, lo, idx)) h->table[off + (idx >> 5)] |= 1u << (idx & 31u);
+            for (uint32_t i = lo; i < lo + n; ++i) h->info[h->ninfo + i] = j | (lo << 8) | (n << 18) | (off << 22);
+            h->ulo[h->nunits] = lo;
+            h->un[h->nunits] = n;
+            h->uoff[h->nunits] = off;
+            ++h->nunits;
+        }
+        if (!ok) break;
+        h->ninfo += nlow;
+        ++h->L;
+        if (k == 1u) break; /* the root */
+        for (uint32_t x = 0; x < nt; ++x) unit_of[x] = -1;
+        for (uint32_t j = 0; j < k; ++j) unit_of[roots[j]] = (int)j;
+        nlow = k;
+    }
+    free(t);
+    free(st);
+    free(unit_of);
+    free(roots);
+    free(cnt);
+    free(first);
+    if (!ok) hplan_free(h);
+    return ok;
+}
+
+/* index bits [lo, lo + n) of the words vec[0..nwv) into `idx` (static lo) */
+static void h_emit_extract_static(Buf* b, const char* vec, uint32_t nwv, uint32_t lo, uint32_t n, int indent) {
+    const uint32_t w = lo / 32u, sh = lo % 32u;
+    if (sh + n <= 32u || w + 1u >= nwv)
+        bput(b, "%*sidx = (%s[%u] >> %u) & 0x%xu;\n", indent, "", vec, w, sh, (1u << n) - 1u);
+    else
+        bput(b, "%*sidx = (uint32_t)((((uint64_t)%s[%u] << 32) | %s[%u]) >> %u) & 0x%xu;\n", indent, "", vec, w + 1u,
+             vec, w, sh, (1u << n) - 1u);
+}
+
+/* the full evaluation: every level's unit values from bits[], the root into r */
+static void hlut_emit_init(Buf* b, const HPlan* h, uint32_t nw, int indent) {
+    bput(b, "%*suint32_t idx;\n", indent, "");
+    for (uint32_t L = 0; L < h->L; ++L) {
+        char lowv[16];
+        snprintf(lowv, sizeof lowv, L ? "hv%u" : "bits", L - 1u);
+        const uint32_t nwl = L ? (h->k[L - 1] + 31u) / 32u : 0u;
+        const uint32_t last = L + 1u == h->L;
+        if (!last)
+            for (uint32_t w = 0; w < (h->k[L] + 31u) / 32u; ++w) bput(b, "%*shv%u[%u] = 0u;\n", indent, "", L, w);
+        for (uint32_t j = 0; j < h->k[L]; ++j) {
+            const uint32_t u = h->ubase[L] + j;
+            h_emit_extract_static(b, lowv, L ? nwl : nw, h->ulo[u], h->un[u], indent);
+            if (last)
+                bput(b, "%*sr = (WO_HTAB[%uu + (idx >> 5)] >> (idx & 31u)) & 1u;\n", indent, "", h->uoff[u]);
+            else
+                bput(b, "%*shv%u[%u] |= ((WO_HTAB[%uu + (idx >> 5)] >> (idx & 31u)) & 1u) << %u;\n", indent, "", L,
+                     j / 32u, h->uoff[u], j % 32u);
+        }
+    }
+}
+
+/* one event's update: primitive `ord`'s unit at each level, the root into r */
+static void hlut_emit_update(Buf* b, const HPlan* h, uint32_t nw, int indent) {
+    bput(b, "%*suint32_t hi = ord;\n", indent, "");
+    for (uint32_t L = 0; L < h->L; ++L) {
+        const uint32_t nwl = L ? (h->k[L - 1] + 31u) / 32u : nw;
+        char lowv[16];
+        snprintf(lowv, sizeof lowv, L ? "hv%u" : "bits", L - 1u);
+        bput(b, "%*s{\n", indent, "");
+        bput(b,
+             "%*s  const uint32_t e = WO_HINFO[%uu + hi];\n"
+             "%*s  const uint32_t lo = (e >> 8) & 0x3ffu, n = (e >> 18) & 0xfu;\n",
+             indent, "", h->base[L], indent, "");
+        if (nwl == 1u) {
+            bput(b, "%*s  const uint32_t idx = (%s[0] >> lo) & ((1u << n) - 1u);\n", indent, "", lowv);
+        } else {
+            bput(b, "%*s  const uint32_t w = lo >> 5;\n%*s  uint32_t a0 = %s[0], a1 = %s[1];\n", indent, "", indent, "",
+                 lowv, lowv);
+            for (uint32_t k = 1; k < nwl; ++k) {
+                bput(b, "%*s  a0 = w == %uu ? %s[%u] : a0;\n", indent, "", k, lowv, k);
+                if (k + 1u < nwl) bput(b, "%*s  a1 = w == %uu ? %s[%u] : a1;\n", indent, "", k, lowv, k + 1u);
+            }
+            bput(b, "%*s  const uint32_t idx = (uint32_t)((((uint64_t)a1 << 32) | a0) >> (lo & 31u)) & ((1u << n) - 1u);\n",
+                 indent, "");
+        }
+        bput(b, "%*s  const uint32_t v = (WO_HTAB[(e >> 22) + (idx >> 5)] >> (idx & 31u)) & 1u;\n", indent, "");
+        if (L + 1u == h->L) {
+            bput(b, "%*s  r = v;\n", indent, "");
+        } else {
+            bput(b, "%*s  const uint32_t j = e & 0xffu, jm = 1u << (j & 31u);\n", indent, "");
+            for (uint32_t w = 0; w < (h->k[L] + 31u) / 32u; ++w)
+                bput(b, "%*s  hv%u[%u] = (j >> 5) == %uu ? ((hv%u[%u] & ~jm) | (v ? jm : 0u)) : hv%u[%u];\n", indent, "", L,
+                     w, w, L, w, L, w);
+            bput(b, "%*s  hi = j;\n", indent, "");
+        }
+        bput(b, "%*s}\n", indent, "");
+    }
+}
+
 char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prims) {
     Buf b = {0};
     Gen g;
@@ -1649,6 +1875,13 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     } else {
         bput(&b, "#define WO_JIT_LUT 0\n");
     }
+    /* levels of truth tables for a general tree above lut_plan's size (hlut_plan;
+     * a chain has too many levels and keeps its decision lists) */
+    HPlan hl;
+    memset(&hl, 0, sizeof hl);
+    const int use_hlut =
+        n_prims > 64u && !g.term_mode && !n_uterms && !use_lut && hlut_plan(prog, n_recs, n_prims, &hl);
+    bput(&b, "#define WO_JIT_HLUT %d\n", use_hlut);
     /* A full LDS event list keeps its smallest keys (WO_LDS_KEEP_SMALLEST): csg32_nested
      * 20.18 -> 10.97 ms (re-collects per segment 0.86 -> 0.18).  A union of small
      * terms (csg32, csg256 balanced) rarely fills the list, and there the eviction
@@ -1670,7 +1903,10 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * (csg256 balanced 9.98 / 9.32 / 10.00 ms at 4 / 5 / 6); 8 for the truth-table form
      * (csg32_nested 9.64 / 9.33 / 9.07 at 4 / 5 / 6, with the cull barrier 9.01 / 8.91 / 8.89
      * at 6 / 7 / 8). */
-    bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW %d\n#endif\n", use_lut ? 8 : 5);
+    /* 14 for the levelled tables' big trees (csg360_nested with the flat evaluation:
+     * 250.7 / 243.9 / 235.7 ms at 10 / 12 / 14 events and 5 waves per SIMD, 241.5 at 16
+     * and 4 waves; 304.6 at 5 and 8 waves) */
+    bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW %d\n#endif\n", use_lut ? 8 : use_hlut ? 14 : 5);
     if (g.term_mode) bput(&b, "// term mode: %u terms (%u outside the spatial hierarchy)\n", n_jterms, g.ntunb);
     /* small scenes run 8 waves per SIMD: a 7-entry LDS list keeps 8 workgroups'
      * LDS within the CU (csg32 5.24 -> 5.19 ms; csg256 balanced keeps 8 entries:
@@ -1717,6 +1953,15 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          * the LDS occupancy) */
         bput(&b, "#define WO_UTERM kUTerm\n");
     }
+    if (use_hlut) {
+        bput(&b, "// root by %u levels of truth tables (units per level:", hl.L);
+        for (uint32_t L = 0; L < hl.L; ++L) bput(&b, " %u", hl.k[L]);
+        bput(&b, ")\n__constant__ uint32_t kHInfo[%u] = {", hl.ninfo);
+        for (uint32_t i = 0; i < hl.ninfo; ++i) bput(&b, "%s0x%08xu", i ? ", " : "", hl.info[i]);
+        bput(&b, "};\n__constant__ uint32_t kHTab[%u] = {", hl.words);
+        for (uint32_t i = 0; i < hl.words; ++i) bput(&b, "%s0x%08xu", i ? ", " : "", hl.table[i]);
+        bput(&b, "};\n");
+    }
     bput(&b, "__constant__ uint32_t kOrdPc[%u] = {", n_prims ? n_prims : 1u);
     if (!n_prims) bput(&b, "0u");
     for (uint32_t i = 0, o = 0; i < n_recs; ++i)
@@ -1733,6 +1978,12 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "#if WO_JIT_LUT\n"
          "  const __attribute__((address_space(3))) uint32_t* lut;  // LDS copy of kLut\n"
          "#define WO_LUT lut\n"
+         "#endif\n"
+         "#if WO_JIT_HLUT\n"
+         "  const __attribute__((address_space(3))) uint32_t* hinfo;  // LDS copies of kHInfo / kHTab\n"
+         "  const __attribute__((address_space(3))) uint32_t* htab;\n"
+         "#define WO_HINFO hinfo\n"
+         "#define WO_HTAB htab\n"
          "#endif\n"
          "  __device__ __forceinline__ WoRec hit_leaf(const wodev::Hit& h) const {\n"
          "    return prog[ordpc[h.ord()] + 1u + h.member()];\n"
@@ -1852,6 +2103,51 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
         if (n_uterms) {
             gen_union_sweep(&g, uterms, n_uterms, n_recs, nw);
             eval_ops = 12u + 2u * (nw - 1u);
+        } else if (use_hlut) {
+            bput(&b, "    ");
+            for (uint32_t L = 0; L + 1u < hl.L; ++L) bput(&b, "uint32_t hv%u[%u]; ", L, (hl.k[L] + 31u) / 32u);
+            bput(&b, "// WO_STATE_DECL\n"
+                     "    uint32_t r;\n"
+                     "    // WO_EVAL_BEGIN (every level's units from bits[], the root into r; tests/test_jit.py)\n"
+                     "    {\n");
+            hlut_emit_init(&b, &hl, nw, 6);
+            bput(&b,
+                 "    }\n"
+                 "    // WO_EVAL_END\n"
+                 "    for (;;) {\n"
+                 "      if (have & (r != root)) { wodev::hit_from_key(key, r, hit); return true; }\n"
+                 "      root = r;\n"
+                 "      if (!win.next(key)) {  // key keeps the last processed event\n"
+                 "        if (!win.dropped()) return false;\n"
+                 "        after = key;\n"
+                 "        WO_WK(WO_WORK_RECOLLECTS);\n"
+                 "        win.clear();\n"
+                 "        {\n");
+            g.first_pass = 0;
+            gen_collect_all(&g, 10);
+            bput(&b,
+                 "        }\n"
+                 "        if (!win.next(key)) return false;\n"
+                 "      }\n"
+                 "      have = true;\n"
+                 "      WO_WK(WO_WORK_SWEEP_STEPS);\n"
+                 "      WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);\n"
+                 "      // WO_TOGGLE_BEGIN (the event's membership toggle and its units' update; tests/test_jit.py)\n"
+                 "      {\n"
+                 "        uint32_t ord = ((uint32_t)key) >> 12;\n"
+                 "        uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n");
+            for (uint32_t w = 0; w < nw; ++w) bput(&b, "        bits[%u] ^= w == %uu ? m : 0u;\n", w, w);
+            hlut_emit_update(&b, &hl, nw, 8);
+            bput(&b,
+                 "      }\n"
+                 "      // WO_TOGGLE_END\n"
+                 "    }\n"
+                 "  }\n"
+                 "};\n");
+            /* per level: the entry's read and fields, the index (a word select per lower
+             * word), the table read and bit, the unit's bit set */
+            eval_ops = 0;
+            for (uint32_t L = 0; L < hl.L; ++L) eval_ops += 12u + 2u * ((L ? (hl.k[L - 1] + 31u) / 32u : nw) - 1u);
         } else {
             bput(&b,
                  "    for (;;) {\n"
@@ -1919,7 +2215,7 @@ kernel_tail:
     bput(&b,
          "\n#ifndef WO_JIT_MIN_WAVES\n"
          "#define WO_JIT_MIN_WAVES %u\n#endif\n",
-         n_uterms ? 7u : (n_prims > 64u || g.lds_events) ? 8u : 7u);
+         n_uterms ? 7u : use_hlut ? 5u : (n_prims > 64u || g.lds_events) ? 8u : 7u);
     bput(&b,
          "extern \"C\" __global__ __launch_bounds__(256, WO_JIT_MIN_WAVES) void wo_jit_pathtrace(\n"
          "    const WoRec* __restrict__ prog, const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t local_rows,\n"
@@ -1935,6 +2231,13 @@ kernel_tail:
          "  __shared__ uint32_t s_lut[sizeof(kLut) / 4];\n"
          "  for (uint32_t i = threadIdx.x; i < sizeof(kLut) / 4; i += wodev::kBlock) s_lut[i] = kLut[i];\n"
          "  tr.lut = (const __attribute__((address_space(3))) uint32_t*)s_lut;\n"
+         "#endif\n"
+         "#if WO_JIT_HLUT\n"
+         "  __shared__ uint32_t s_hinfo[sizeof(kHInfo) / 4], s_htab[sizeof(kHTab) / 4];\n"
+         "  for (uint32_t i = threadIdx.x; i < sizeof(kHInfo) / 4; i += wodev::kBlock) s_hinfo[i] = kHInfo[i];\n"
+         "  for (uint32_t i = threadIdx.x; i < sizeof(kHTab) / 4; i += wodev::kBlock) s_htab[i] = kHTab[i];\n"
+         "  tr.hinfo = (const __attribute__((address_space(3))) uint32_t*)s_hinfo;\n"
+         "  tr.htab = (const __attribute__((address_space(3))) uint32_t*)s_htab;\n"
          "#endif\n"
          "#if WO_JIT_LDS_PROG  // hit-leaf and material reads from LDS (pathtrace_block's first barrier orders the copy)\n"
          "  __shared__ WoRec s_prog[%u];\n"
@@ -1965,6 +2268,7 @@ kernel_tail:
     bput(&b, "// wo_share_tiles %u\n", 3u);
     free(g.dls);
     free(lut.table);
+    hplan_free(&hl);
     free(uterms);
     free(sprims);
     free(tunb);

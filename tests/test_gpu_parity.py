@@ -69,6 +69,9 @@ def test_ubershader_kats_on_gpu(empty_renderer):
 
 
 PATHS = ["jit", "interpreter", "lanes"]
+# csg360_nested's specialised kernel (levelled truth tables, ~300 primitives) takes hiprtc
+# a minute or two the first time a process builds it
+CSG360 = pytest.param("csg360_nested", marks=pytest.mark.timeout(600))
 
 
 def _scene(name, path="jit", **kw):
@@ -142,8 +145,12 @@ def _check_path(r, path, scene=None):
         want = "interpreter"
     elif path == "lanes" and _lanes_eligible(r):
         want = "lanes"
-    else:  # JIT up to WOLOLO_JIT_MAX_PRIMS (256) primitives; above, the lanes (rtiow_cover's 487, csg360_nested's 309)
-        want = "jit" if 0 < nprim <= 256 else ("lanes" if _lanes_eligible(r) else "interpreter")
+    else:
+        # JIT up to WOLOLO_JIT_MAX_PRIMS (256) primitives, and above for a general tree the
+        # levelled truth tables evaluate (csg360_nested's 309); else the lanes (rtiow_cover's
+        # 487, csg512_balanced's union of terms)
+        hlut = nprim > 256 and "#define WO_JIT_HLUT 1\n" in (r.jit_source() or "")
+        want = "jit" if (0 < nprim <= 256 or hlut) else ("lanes" if _lanes_eligible(r) else "interpreter")
     assert r.trace_path() == want, (scene, r.trace_path(), want)
 
 
@@ -157,7 +164,7 @@ def _oracle_rows(r, params):
 
 @pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("scene", ["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain",
-                                   "csg512_balanced", "csg360_nested"])
+                                   "csg512_balanced", CSG360])
 @pytest.mark.parametrize("mode", [wl.MODE_PATHTRACE, wl.MODE_NORMALS])
 def test_pathtrace_small_frame_bitexact(scene, mode, path):
     r, info = _scene(scene, path)
@@ -172,7 +179,7 @@ def test_pathtrace_small_frame_bitexact(scene, mode, path):
 
 @pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("scene", ["csg32", "csg32_nested", "rtiow_cover", "csg256_balanced", "csg256_chain",
-                                   "csg512_balanced", "csg360_nested"])
+                                   "csg512_balanced", CSG360])
 def test_pathtrace_full_size_sampled_pixels(scene, path):
     """BASELINE configs at full size (1920x1080, 64 spp, 8 bounces): the whole frame on
     the GPU, a random sample of pixels on the oracle.  Every path runs every scene (the
@@ -545,13 +552,17 @@ def test_lane_tracer_forms_bitexact(scene, monkeypatch):
     r.close()
 
 
-def test_auto_tracer_choices():
+@pytest.mark.timeout(600)
+def test_auto_tracer_choices(monkeypatch):
     """AUTO: the RTIOW cover (union-only, 487 primitives) takes the lane tracer; csg32 and a
     128-primitive union-only scene the JIT; csg512_balanced (427 primitives, a union of
     small terms) the lane tracer's resumable 4-wide term-mode walk; csg360_nested (309
-    primitives of a general tree) its general form."""
+    primitives of a general tree) the JIT with levelled truth tables, or with
+    WOLOLO_JIT_GENERAL=0 the lane tracer's general form."""
     for name, want in [("rtiow_cover", "lanes"), ("csg32", "jit"), ("csg256_balanced_union", "jit"),
-                       ("csg512_balanced", "lanes"), ("csg360_nested", "lanes")]:
+                       ("csg512_balanced", "lanes"), ("csg360_nested", "jit"), ("csg360_nested", "lanes")]:
+        if name == "csg360_nested" and want == "lanes":
+            monkeypatch.setenv("WOLOLO_JIT_GENERAL", "0")  # the lanes' general form instead
         r, info = _scene(name, "auto")
         r.render(info.params(width=32, height=18, spp=1))
         assert r.trace_path() == want, (name, r.trace_path())
@@ -560,9 +571,11 @@ def test_auto_tracer_choices():
         if name == "csg512_balanced":
             # > 256 terms: the resumable 4-wide walk in term mode (kLanesDynWideTerms)
             assert r.lanes_info()["kind"] == 14, r.lanes_info()
-        if name == "csg360_nested":
-            # > 256 primitives of a general tree: kLanesGeneral
-            assert r.lanes_info()["kind"] == 7, r.lanes_info()
+        if name == "csg360_nested" and want == "jit":
+            # > 256 primitives of a general tree: the specialised kernel's levelled truth tables
+            assert "#define WO_JIT_HLUT 1" in r.jit_source()
+        if name == "csg360_nested" and want == "lanes":
+            assert r.lanes_info()["kind"] == 7, r.lanes_info()  # kLanesGeneral
         r.close()
 
 

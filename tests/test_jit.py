@@ -337,14 +337,22 @@ def _compile_sweep(tmp_path, src, nw, ncull, lut=1):
     m = re.search(r"__constant__ uint32_t kLut\[\d+\] = \{.*?\};", src, re.S)
     if m:
         table += m.group(0).replace("__constant__", "static const") + "\n#define WO_LUT kLut\n"
+    for name, macro in (("kHInfo", "WO_HINFO"), ("kHTab", "WO_HTAB")):
+        m = re.search(r"__constant__ uint32_t " + name + r"\[\d+\] = \{.*?\};", src, re.S)
+        if m:
+            table += m.group(0).replace("__constant__", "static const") + f"\n#define {macro} {name}\n"
     table = f"#define WO_JIT_LUT {lut}\n" + table
-    root_after = "(ucnt != 0)" if "kUTerm" in table else None
+    # the levelled tables' unit values persist from the evaluation into the toggles
+    m = re.search(r"^(.*)// WO_STATE_DECL", src, re.M)
+    state = m.group(1) + "\n" if m else ""
+    root_after = "(ucnt != 0)" if "kUTerm" in table else "r" if "kHTab" in table else None
     c = tmp_path / f"ev{lut}.cpp"
     c.write_text("#include <stddef.h>\n#include <stdint.h>\n" + table +
                  "extern \"C\" void run(const uint32_t* all, int n, const uint32_t* ords, int nev, uint32_t* out) {\n"
                  f"  for (int i = 0; i < n; ++i) {{\n    uint32_t bits[{nw}];\n"
                  f"    for (int k = 0; k < {nw}; ++k) bits[k] = all[(size_t)i * {nw} + k];\n"
-                 f"    uint32_t cull[{ncull}] = {{0}};\n    int ucnt = 0; (void)ucnt; bool was = false; (void)was;\n    uint32_t r;\n" + body +
+                 f"    uint32_t cull[{ncull}] = {{0}};\n    int ucnt = 0; (void)ucnt; bool was = false; (void)was;\n    uint32_t r;\n" +
+                 state + body +
                  "    out[(size_t)i * (nev + 1)] = r;\n"
                  "    for (int e = 0; e < nev; ++e) {\n"
                  "      const uint64_t key = (uint64_t)ords[(size_t)i * nev + e] << 12;\n" + toggle +
@@ -357,7 +365,7 @@ def _compile_sweep(tmp_path, src, nw, ncull, lut=1):
 
 
 @pytest.mark.parametrize("case", ["csg32_nested", "csg256_balanced", "csg256_chain", "chain_uud", "chain_uid",
-                                  "chain_d", "random_a", "random_b", "unionpairs"])
+                                  "chain_d", "random_a", "random_b", "unionpairs", "csg360_nested"])
 def test_generated_root_evaluation(hostonly, tmp_path, case):
     """The generated root evaluation of the event-list form (the scenes whose root is
     not a union of small terms: flattened literal sets; decision lists for chains; the
@@ -382,6 +390,8 @@ def test_generated_root_evaluation(hostonly, tmp_path, case):
     if case == "csg32_nested":
         assert "kLut" in src  # two subtrees of <= 12 primitives: the truth-table evaluation
         assert wl.jit_compile_check(src, "gfx950") == ""
+    if case == "csg360_nested":
+        assert "kHTab" in src  # 309 primitives: levels of truth tables, updated per event
     for lut in ((1, 0) if "kLut" in src else (1,)):
         _check_generated_eval(tmp_path, src, prog, nrec, nprim, lut)
 
