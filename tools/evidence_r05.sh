@@ -3,11 +3,16 @@
 # (kernel stats, HBM bytes, instruction mix) for every kernel the bench runs, and
 # rank 0's N-GPU step with the present map-back for every config.  Results under
 # gpurun_out/; tools/pmc_summary.py turns the profiles into profiles/ summaries.
-#   tools/evidence_r05.sh bench|prof1|prof2|rs|rsnomap
+#   tools/evidence_r05.sh bench|prof1|prof2|rs|rsnomap|final
+# (a heartbeat line every 50 s: the specialised kernel of csg360_nested compiles for a
+# minute or two, which the box's silence watchdog would take for a hang)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 S=tools/gpu_session.sh
 B="--no-cpu-baseline --no-draw-frame --side-scenes ''"
+(while sleep 50; do echo "tick $(date +%s)"; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 case "${1:-bench}" in
 bench)
     bash $S \
@@ -17,7 +22,7 @@ bench)
         "b256c:200:python bench.py --scene csg256_chain --steps 10 --warmup 2 $B > gpurun_out/r05_bench_256c.json" \
         "brt:300:python bench.py --scene rtiow_cover --steps 5 --warmup 1 $B > gpurun_out/r05_bench_rtiow.json" \
         "b512:300:python bench.py --scene csg512_balanced --steps 5 --warmup 1 $B > gpurun_out/r05_bench_512b.json" \
-        "b360:300:python bench.py --scene csg360_nested --steps 3 --warmup 1 $B > gpurun_out/r05_bench_csg360.json" \
+        "b360:600:python bench.py --scene csg360_nested --steps 3 --warmup 1 $B > gpurun_out/r05_bench_csg360.json" \
         "bc4:300:python bench.py --width 3840 --height 2160 --spp 256 --steps 3 --warmup 1 $B > gpurun_out/r05_bench_c4.json"
     ;;
 prof1)
@@ -42,6 +47,15 @@ rs)
         "rsrt:300:python tools/root_step.py --scene rtiow_cover --worlds 2 4 8 --map-back bgra > gpurun_out/r05_root_step_rtiow.log 2>&1" \
         "rs512:300:python tools/root_step.py --scene csg512_balanced --worlds 2 4 8 --map-back bgra > gpurun_out/r05_root_step_512b.log 2>&1" \
         "rsc4:400:python tools/root_step.py --scene csg32 --width 3840 --height 2160 --spp 256 --worlds 2 4 8 --map-back bgra > gpurun_out/r05_root_step_c4.log 2>&1"
+    ;;
+final)
+    # the round's last build: every bench line, then the headline's, the nested tree's and
+    # csg360's profiles (csg360_nested now takes the specialised kernel)
+    bash "$0" bench || exit $?
+    bash $S \
+        "p32:400:bash tools/profile_session.sh r05f_csg32 --steps 20 --warmup 3" \
+        "p32n:400:bash tools/profile_session.sh r05f_csg32_nested --scene csg32_nested --steps 10 --warmup 2" \
+        "p360:900:bash tools/profile_session.sh r05f_csg360 --scene csg360_nested --steps 3 --warmup 1"
     ;;
 rsnomap)
     # the same without the present map-back (bench.py's N-GPU frame is not presented)
