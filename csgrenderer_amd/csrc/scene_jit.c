@@ -97,6 +97,7 @@ typedef struct Gen {
     uint32_t nsprims;
     struct SPrim* tunb;    /* term mode: terms without a bounding sphere (tested first, ungrouped) */
     uint32_t ntunb;
+    const struct RTree* rtree; /* collect over the CSG tree with relevance-box culls (gen_rtree), or NULL */
     struct DList* dls; /* decision-list pool (ids are 1-based; 0 = none) */
     uint32_t ndl, dl_cap;
     int err;
@@ -512,12 +513,16 @@ static void gen_cull_barrier(Gen* g, int indent) {
     bput(g->b, "#endif\n");
 }
 
+static void gen_rtree(Gen* g, int indent);
+
 /* the collect of the whole program (either pass) */
 static void gen_collect_all(Gen* g, int indent) {
     if (!g->first_pass) gen_cull_barrier(g, indent);
     g->nbound = 0;
     if (g->term_mode)
         gen_collect_terms(g, indent);
+    else if (g->rtree)
+        gen_rtree(g, indent);
     else if (g->spatial)
         gen_collect_spatial(g, g->sprims, g->nsprims, indent);
     else
@@ -1671,6 +1676,248 @@ static void hlut_emit_update(Buf* b, const HPlan* h, uint32_t nw, int indent) {
     }
 }
 
+/* ---- collect over the CSG tree, culled by relevance boxes ----
+ * For a general tree (the levelled tables' scenes) the primitives are collected
+ * in a walk of the tree itself, and a subtree of >= WO_RCULL_MIN primitives gets a
+ * wave-level test of the sphere around its box: the meet of its bounds (a union's
+ * hull, an intersection's meet, a difference's left operand's) with its relevance
+ * box (the meet of the bounds of the operands that gate it on its path to the
+ * root -- an intersection's other operand, a difference's left one for its right
+ * one).  A wave whose rays all miss it skips the subtree: along those rays the
+ * subtree is either empty or gated off wherever it is not, so its bits staying 0
+ * leaves the root's value, and the hit, unchanged (the lane tracer's relevance
+ * argument).  A subtree whose box is empty is never collected. */
+typedef struct RBox {
+    double lo[3], hi[3];
+} RBox;
+typedef struct RSph {
+    double c[3], r; /* r < 0: none (unbounded) */
+} RSph;
+typedef struct RTree {
+    TNode* t;
+    int root;
+    RBox *bnd, *rel;
+    RSph* sph; /* per node: a sphere around its bounds (tighter than the box's for unions of spheres) */
+    uint32_t* pc_of; /* per ordinal: its PRIM record */
+    uint32_t cull_min;
+} RTree;
+
+static RBox rb_inf(void) {
+    RBox b;
+    for (int a = 0; a < 3; ++a) b.lo[a] = -INFINITY, b.hi[a] = INFINITY;
+    return b;
+}
+static RBox rb_meet(RBox x, RBox y) {
+    for (int a = 0; a < 3; ++a) x.lo[a] = fmax(x.lo[a], y.lo[a]), x.hi[a] = fmin(x.hi[a], y.hi[a]);
+    return x;
+}
+static RBox rb_hull(RBox x, RBox y) {
+    for (int a = 0; a < 3; ++a) x.lo[a] = fmin(x.lo[a], y.lo[a]), x.hi[a] = fmax(x.hi[a], y.hi[a]);
+    return x;
+}
+static RBox rb_slack(RBox x, double k) {
+    for (int a = 0; a < 3; ++a) {
+        if (!isfinite(x.lo[a]) || !isfinite(x.hi[a])) continue;
+        const double m = k * (1e-4 * (fabs(x.lo[a]) + fabs(x.hi[a]) + fabs(x.hi[a] - x.lo[a])) + 1e-5);
+        x.lo[a] -= m;
+        x.hi[a] += m;
+    }
+    return x;
+}
+static int rb_empty(const RBox* x) {
+    for (int a = 0; a < 3; ++a)
+        if (x->lo[a] > x->hi[a]) return 1;
+    return 0;
+}
+static int rb_finite(const RBox* x) {
+    for (int a = 0; a < 3; ++a)
+        if (!isfinite(x->lo[a]) || !isfinite(x->hi[a])) return 0;
+    return 1;
+}
+/* a convex primitive's box: sphere members and axis-aligned half-spaces (others: none) */
+static RBox prim_box(const WoRec* prog, uint32_t pc) {
+    RBox b = rb_inf();
+    for (uint32_t m = 0; m < prog[pc].u0; ++m) {
+        const WoRec* L = &prog[pc + 1u + m];
+        if (L->op == WO_LEAF_SPHERE) {
+            const double r = sqrt((double)L->f[3]);
+            for (int a = 0; a < 3; ++a) {
+                b.lo[a] = fmax(b.lo[a], (double)L->f[a] - r);
+                b.hi[a] = fmin(b.hi[a], (double)L->f[a] + r);
+            }
+        } else if (L->op == WO_LEAF_HALFSPACE && L->u1 >= 1u && L->u1 <= 3u) {
+            const int a = (int)L->u1 - 1; /* s * x_a <= h */
+            if (L->f[a] > 0.0f)
+                b.hi[a] = fmin(b.hi[a], (double)L->f[3]);
+            else
+                b.lo[a] = fmax(b.lo[a], -(double)L->f[3]);
+        }
+    }
+    return b;
+}
+
+/* the smallest sphere enclosing two spheres */
+static RSph rs_hull(RSph a, RSph b) {
+    if (a.r < 0.0 || b.r < 0.0) {
+        RSph u = {{0.0, 0.0, 0.0}, -1.0};
+        return u;
+    }
+    double d[3], l = 0.0;
+    for (int k = 0; k < 3; ++k) d[k] = b.c[k] - a.c[k], l += d[k] * d[k];
+    l = sqrt(l);
+    if (l + b.r <= a.r) return a;
+    if (l + a.r <= b.r) return b;
+    RSph h;
+    h.r = 0.5 * (l + a.r + b.r);
+    for (int k = 0; k < 3; ++k) h.c[k] = a.c[k] + (l > 0.0 ? d[k] / l * (h.r - a.r) : 0.0);
+    return h;
+}
+/* a convex primitive's sphere: its smallest sphere member (the primitive lies inside each) */
+static RSph prim_sph(const WoRec* prog, uint32_t pc) {
+    RSph s = {{0.0, 0.0, 0.0}, -1.0};
+    for (uint32_t m = 0; m < prog[pc].u0; ++m) {
+        const WoRec* L = &prog[pc + 1u + m];
+        if (L->op != WO_LEAF_SPHERE) continue;
+        const double r = sqrt((double)L->f[3]);
+        if (s.r < 0.0 || r < s.r) s.c[0] = L->f[0], s.c[1] = L->f[1], s.c[2] = L->f[2], s.r = r;
+    }
+    return s;
+}
+
+static void rtree_free(RTree* rt) {
+    free(rt->sph);
+    free(rt->t);
+    free(rt->bnd);
+    free(rt->rel);
+    free(rt->pc_of);
+    memset(rt, 0, sizeof *rt);
+}
+
+static int rtree_build(const WoRec* prog, uint32_t n_recs, uint32_t n_prims, RTree* rt) {
+    memset(rt, 0, sizeof *rt);
+    const uint32_t cap = 2u * n_prims;
+    rt->t = (TNode*)malloc(sizeof(TNode) * cap);
+    rt->bnd = (RBox*)malloc(sizeof(RBox) * cap);
+    rt->rel = (RBox*)malloc(sizeof(RBox) * cap);
+    rt->pc_of = (uint32_t*)malloc(sizeof(uint32_t) * n_prims);
+    rt->sph = (RSph*)malloc(sizeof(RSph) * cap);
+    int* st = (int*)malloc(sizeof(int) * (n_prims + 1u));
+    int ok = rt->t && rt->bnd && rt->rel && rt->pc_of && rt->sph && st && n_prims > 0u;
+    uint32_t nt = 0, sp = 0;
+    for (uint32_t pc = 0; pc < n_recs && ok;) {
+        const WoRec* r = &prog[pc];
+        if (r->op == WO_OP_PRIM) {
+            ok = nt < cap && sp <= n_prims && r->u1 < n_prims;
+            if (!ok) break;
+            TNode x = {0, -1, -1, r->u1, 1u};
+            rt->pc_of[r->u1] = pc;
+            rt->bnd[nt] = prim_box(prog, pc);
+            rt->sph[nt] = prim_sph(prog, pc);
+            rt->t[nt] = x;
+            st[sp++] = (int)nt++;
+            pc += 1u + r->u0;
+            continue;
+        }
+        ++pc;
+        if (r->op == WO_OP_BOUND) continue;
+        ok = sp >= 2u && nt < cap;
+        if (!ok) break;
+        const int b = st[--sp], a = st[--sp];
+        TNode x = {(int)r->op, a, b, rt->t[a].lo < rt->t[b].lo ? rt->t[a].lo : rt->t[b].lo, rt->t[a].n + rt->t[b].n};
+        rt->bnd[nt] = r->op == WO_OP_UNION   ? rb_hull(rt->bnd[a], rt->bnd[b])
+                      : r->op == WO_OP_INTER ? rb_meet(rt->bnd[a], rt->bnd[b])
+                      : r->op == WO_OP_DIFF  ? rt->bnd[a]
+                                             : rt->bnd[b]; /* RDIFF: b AND NOT a */
+        {
+            const RSph sa = rt->sph[a], sb = rt->sph[b];
+            if (r->op == WO_OP_UNION)
+                rt->sph[nt] = rs_hull(sa, sb);
+            else if (r->op == WO_OP_INTER) /* inside both: the smaller bounded one */
+                rt->sph[nt] = sa.r < 0.0 ? sb : (sb.r < 0.0 || sa.r <= sb.r ? sa : sb);
+            else
+                rt->sph[nt] = r->op == WO_OP_DIFF ? sa : sb;
+        }
+        rt->t[nt] = x;
+        st[sp++] = (int)nt++;
+    }
+    ok = ok && sp == 1u;
+    if (ok) {
+        rt->root = st[0];
+        rt->rel[rt->root] = rb_inf();
+        /* a node before its operands: postfix order reversed */
+        for (uint32_t i = nt; i-- > 0;) {
+            const TNode* x = &rt->t[i];
+            if (x->op == 0) continue;
+            const RBox c = rt->rel[i];
+            const int a = x->l, b = x->r;
+            rt->rel[a] = x->op == WO_OP_INTER || x->op == WO_OP_RDIFF ? rb_meet(c, rt->bnd[b]) : c;
+            rt->rel[b] = x->op == WO_OP_INTER || x->op == WO_OP_DIFF ? rb_meet(c, rt->bnd[a]) : c;
+        }
+    }
+    free(st);
+    if (!ok) rtree_free(rt);
+    return ok;
+}
+
+static void gen_rtree_node(Gen* g, int x, int indent) {
+    const RTree* rt = g->rtree;
+    const TNode* n = &rt->t[x];
+    const RBox m = rb_meet(rb_slack(rt->bnd[x], 2.0), rb_slack(rt->rel[x], 2.0));
+    if (rb_empty(&m)) return; /* never matters: its bits stay 0 */
+    if (n->op == 0) {
+        const uint32_t pc = rt->pc_of[n->lo];
+        gen_collect(g, pc, pc + 1u + g->prog[pc].u0, indent);
+        return;
+    }
+    int inner = indent;
+    const int test = n->n >= rt->cull_min && rb_finite(&m);
+    if (test) {
+        double c[3], r2 = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            c[a] = 0.5 * (m.lo[a] + m.hi[a]);
+            const double h = 0.5 * (m.hi[a] - m.lo[a]);
+            r2 += h * h;
+        }
+        double R = sqrt(r2) * (1.0 + 1e-6) + 1e-6;
+        const RSph ns = rt->sph[x];
+        if (ns.r >= 0.0) { /* the node's own sphere (it encloses the bounds, so their meet with the relevance box) when smaller */
+            const double nr = ns.r * (1.0 + 2e-4) + 2e-5; /* the BOUND records' slack */
+            if (nr < R) {
+                R = nr;
+                for (int a = 0; a < 3; ++a) c[a] = ns.c[a];
+            }
+        }
+        const uint32_t k = g->nbound++;
+        if (g->first_pass) {
+            const float fc[3] = {(float)c[0], (float)c[1], (float)c[2]};
+            const float fR = (float)(R * (1.0 + 1e-6)), fR2 = (float)(R * R * (1.0 + 4e-6));
+            uint32_t vr2 = fbits(fR2);
+            static const char* nr[1] = {"bc3"};
+            bput(g->b, "%*s{  // relevance group %u (%u primitives)\n%*s  WO_WK(WO_WORK_BOUND_TESTS);\n", indent, "", k,
+                 n->n, indent, "");
+            emit_consts(g->b, indent + 2, "float", nr, &vr2, 1);
+            bput(g->b,
+                 "%*s  float ox, oy, oz, tca, d2, tr;\n"
+                 "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(ox) : \"v\"(o.x));\n"
+                 "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oy) : \"v\"(o.y));\n"
+                 "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oz) : \"v\"(o.z));\n"
+                 "%*s  wodev::bound_tca_d2(ox, oy, oz, d, tca, d2);\n"
+                 "%*s  asm(\"v_add_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(tr) : \"v\"(tca));\n"
+                 "%*s  const bool miss = (d2 > __builtin_fmaf(4e-6f * tca, tca, bc3)) | (tr < 0.0f);\n"
+                 "%*s  if (__ballot(!miss) == 0ull) cull[%u] |= %uu;\n%*s}\n",
+                 indent, "", indent, "", fbits(fc[0]), indent, "", fbits(fc[1]), indent, "", fbits(fc[2]), indent, "",
+                 indent, "", fbits(fR), indent, "", indent, "", k / 32, 1u << (k % 32), indent, "");
+        }
+        bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
+        inner = indent + 2;
+    }
+    gen_rtree_node(g, n->l, inner);
+    gen_rtree_node(g, n->r, inner);
+    if (test) bput(g->b, "%*s}\n", indent, "");
+}
+
+static void gen_rtree(Gen* g, int indent) { gen_rtree_node(g, g->rtree->root, indent); }
+
 char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prims) {
     Buf b = {0};
     Gen g;
@@ -1698,6 +1945,10 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * ms).  Leaves: median splits, chain 15.04 / 13.93 / 13.63 ms at 2 / 4 / 8; SAH,
      * csg32 3.687 / 3.612 / 3.628 / 3.589 at 3 / 4 / 6 / 8. */
     g.spatial = !g.lds_events || n_prims <= 64u;
+    {
+        const char* sp = getenv("WOLOLO_JIT_SPATIAL"); /* (measurement) 1 / 0 forces the spatial collect on / off */
+        if (sp && (*sp == '0' || *sp == '1')) g.spatial = *sp == '1';
+    }
     g.spatial_leaf = 8;
     /* term mode: where the root allows it, the tree is shallow enough for the
      * event-list path it replaces, and the scene is small enough for the spatial
@@ -1842,19 +2093,6 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             free(scratch.s);
         }
     }
-    for (uint32_t i = 0; i < n_recs && !g.term_mode; ++i) nbounds += prog[i].op == WO_OP_BOUND && bound_tested(&g, i);
-
-    bput(&b, "// generated by scene_jit.c: %u records, %u primitives, %u bounds\n", n_recs, n_prims, nbounds);
-    /* Small programs are copied to LDS per workgroup with the materials they use:
-     * the hit leaf / material reads then cost an LDS round trip instead of
-     * dependent global loads.  Larger ones stay in global memory, where the LDS
-     * would cost occupancy. */
-    uint32_t n_mats_used = 1;
-    for (uint32_t i = 0; i < n_recs; ++i)
-        if ((prog[i].op == WO_LEAF_SPHERE || prog[i].op == WO_LEAF_HALFSPACE) && prog[i].u0 + 1u > n_mats_used)
-            n_mats_used = prog[i].u0 + 1u;
-    const int lds_prog =
-        (size_t)n_recs * sizeof(WoRec) + (size_t)n_mats_used * sizeof(WoMaterial) + 4u * n_prims <= 6144u;
     /* the incremental union count's term table, per primitive: its term's mask test */
     uint32_t n_uterms = 0, eval_ops = 0;
     UTerm* uterms = NULL;
@@ -1870,17 +2108,52 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     LutPlan lut;
     memset(&lut, 0, sizeof lut);
     const int use_lut = n_prims && !g.term_mode && !n_uterms && lut_plan(prog, n_recs, n_prims, &lut);
-    if (use_lut) {
-        bput(&b, "#ifndef WO_JIT_LUT\n#define WO_JIT_LUT 1\n#endif\n");
-    } else {
-        bput(&b, "#define WO_JIT_LUT 0\n");
-    }
     /* levels of truth tables for a general tree above lut_plan's size (hlut_plan;
      * a chain has too many levels and keeps its decision lists) */
     HPlan hl;
     memset(&hl, 0, sizeof hl);
     const int use_hlut =
         n_prims > 64u && !g.term_mode && !n_uterms && !use_lut && hlut_plan(prog, n_recs, n_prims, &hl);
+    /* the levelled tables' trees collect over the tree with relevance-box culls
+     * (gen_rtree; WO_RCULL_MIN primitives per tested subtree, 0 = off) */
+    RTree rtree;
+    memset(&rtree, 0, sizeof rtree);
+    {
+        const char* rc = getenv("WOLOLO_JIT_RCULL"); /* (measurement) subtree size tested, 0: off */
+        const uint32_t cull_min = rc && *rc ? (uint32_t)strtoul(rc, NULL, 10) : 2u;
+        if (use_hlut && !g.spatial && cull_min && rtree_build(prog, n_recs, n_prims, &rtree)) {
+            rtree.cull_min = cull_min;
+            g.rtree = &rtree;
+            Buf scratch = {0};
+            Buf* keep = g.b;
+            g.b = &scratch;
+            g.nbound = 0;
+            g.first_pass = 1;
+            gen_rtree(&g, 0);
+            nbounds += g.nbound;
+            g.b = keep;
+            free(scratch.s);
+        }
+    }
+    if (!g.rtree)
+        for (uint32_t i = 0; i < n_recs && !g.term_mode; ++i) nbounds += prog[i].op == WO_OP_BOUND && bound_tested(&g, i);
+
+    bput(&b, "// generated by scene_jit.c: %u records, %u primitives, %u bounds\n", n_recs, n_prims, nbounds);
+    /* Small programs are copied to LDS per workgroup with the materials they use:
+     * the hit leaf / material reads then cost an LDS round trip instead of
+     * dependent global loads.  Larger ones stay in global memory, where the LDS
+     * would cost occupancy. */
+    uint32_t n_mats_used = 1;
+    for (uint32_t i = 0; i < n_recs; ++i)
+        if ((prog[i].op == WO_LEAF_SPHERE || prog[i].op == WO_LEAF_HALFSPACE) && prog[i].u0 + 1u > n_mats_used)
+            n_mats_used = prog[i].u0 + 1u;
+    const int lds_prog =
+        (size_t)n_recs * sizeof(WoRec) + (size_t)n_mats_used * sizeof(WoMaterial) + 4u * n_prims <= 6144u;
+    if (use_lut) {
+        bput(&b, "#ifndef WO_JIT_LUT\n#define WO_JIT_LUT 1\n#endif\n");
+    } else {
+        bput(&b, "#define WO_JIT_LUT 0\n");
+    }
     bput(&b, "#define WO_JIT_HLUT %d\n", use_hlut);
     /* A full LDS event list keeps its smallest keys (WO_LDS_KEEP_SMALLEST): csg32_nested
      * 20.18 -> 10.97 ms (re-collects per segment 0.86 -> 0.18).  A union of small
@@ -2269,6 +2542,7 @@ kernel_tail:
     free(g.dls);
     free(lut.table);
     hplan_free(&hl);
+    rtree_free(&rtree);
     free(uterms);
     free(sprims);
     free(tunb);
