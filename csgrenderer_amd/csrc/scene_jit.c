@@ -2114,23 +2114,30 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     memset(&hl, 0, sizeof hl);
     const int use_hlut =
         n_prims > 64u && !g.term_mode && !n_uterms && !use_lut && hlut_plan(prog, n_recs, n_prims, &hl);
-    /* the levelled tables' trees collect over the tree with relevance-box culls
-     * (gen_rtree; WO_RCULL_MIN primitives per tested subtree, 0 = off) */
+    /* The truth tables' trees (general trees that are not chains) collect over the
+     * tree with relevance-box culls (gen_rtree) instead of the scene compiler's BOUND
+     * records or the spatial groups: csg360_nested 201.6 -> 183.5 ms (subtrees of >= 2
+     * primitives tested; 184.3 / 184.7 / 201.5 at >= 3 / 4 / 16, and 195.3 with the
+     * boxes' spheres alone at 8), csg32_nested 8.83 -> 8.47 ms (>= 4; 8.51 / 8.54 / 8.51 /
+     * 8.64 at 3 / 6 / 8 / 12; 8.66 at 2).  The csg256 chain (decision lists, no tables)
+     * keeps its BOUND records: 11.3 against 24.8 ms.  WOLOLO_JIT_RCULL=<n> sets the
+     * smallest subtree tested (measurements), 0 turns the tree collect off. */
     RTree rtree;
     memset(&rtree, 0, sizeof rtree);
     {
-        const char* rc = getenv("WOLOLO_JIT_RCULL"); /* (measurement) subtree size tested, 0: off */
-        const uint32_t cull_min = rc && *rc ? (uint32_t)strtoul(rc, NULL, 10) : 2u;
-        if (use_hlut && !g.spatial && cull_min && rtree_build(prog, n_recs, n_prims, &rtree)) {
+        const char* rc = getenv("WOLOLO_JIT_RCULL");
+        const uint32_t cull_min = rc && *rc ? (uint32_t)strtoul(rc, NULL, 10) : use_hlut ? 2u : 4u;
+        if ((use_hlut || use_lut) && cull_min && rtree_build(prog, n_recs, n_prims, &rtree)) {
             rtree.cull_min = cull_min;
             g.rtree = &rtree;
+            g.spatial = 0;
             Buf scratch = {0};
             Buf* keep = g.b;
             g.b = &scratch;
             g.nbound = 0;
             g.first_pass = 1;
             gen_rtree(&g, 0);
-            nbounds += g.nbound;
+            nbounds = g.nbound; /* (not the spatial groups counted above: unused) */
             g.b = keep;
             free(scratch.s);
         }

@@ -24,9 +24,9 @@ def _leaf_calls(src):
 def test_generated_sources_compile_for_gfx950(hostonly):
     """The three forms the generator picks by scene, each compiled by hiprtc for gfx950:
     the event list with the scene compiler's BOUND records as the culling structure
-    (csg256_balanced: > 64 primitives in a shallow tree), the event list with spatial
-    groups (csg32_nested: a general root over <= 64 primitives, two boxes), and term
-    mode (csg32: a union of <= 2-literal conjunctions)."""
+    (csg256_balanced: > 64 primitives in a shallow tree), the event list collected over
+    the CSG tree with relevance groups (csg32_nested: a general root over <= 64
+    primitives, two boxes), and term mode (csg32: a union of <= 2-literal conjunctions)."""
     # BOUND records: wave-level tests only for subtrees of >= 4 leaves and not around a
     # lone primitive (its member skip is the cheaper test)
     r = wl.Renderer("jit", max_nodes=4096)
@@ -51,15 +51,19 @@ def test_generated_sources_compile_for_gfx950(hostonly):
     log = wl.jit_compile_check(src, "gfx950")
     assert log == "", log
     r.close()
-    # spatial groups: one wave-level test per group, no BOUND record tested; every leaf
-    # still intersected in both passes; the two boxes' axis faces on the fast path
+    # the tree collect with relevance groups (a general tree with truth tables): one
+    # wave-level test per group of >= 4 primitives, no BOUND record or spatial group
+    # tested; every leaf still intersected in both passes (none of csg32_nested's is
+    # outside its relevance box); the two boxes' axis faces on the fast path
     r = wl.Renderer("jit", max_nodes=4096)
     scenes.build("csg32_nested", r)
     prog, nrec, nprim = r.program()
     src = r.jit_source()
     nleaf = sum(1 for i in range(nrec) if prog[i].op in (wl.WO_LEAF_SPHERE, wl.WO_LEAF_HALFSPACE))
-    ngroups = len(re.findall(r"// group \d+ \((\d+) primitives\)", src))  # the first pass tests them
-    assert ngroups >= 2 and "// BOUND" not in src
+    ngroups = len(re.findall(r"// relevance group \d+ \((\d+) primitives\)", src))  # the first pass tests them
+    assert ngroups >= 2 and "// BOUND" not in src and "// group" not in src
+    first = src[:src.index('WO_MARK("collect_end")')]
+    assert len(set(re.findall(r"// primitive (\d+)", first))) == nprim
     assert len(re.findall(r"if \(__ballot\(!miss\) == 0ull\)", src)) == ngroups
     nsingle, npair = _leaf_calls(src)
     assert npair >= 2 * 6  # two boxes: three face pairs each, in both passes
@@ -435,7 +439,7 @@ def _f32(h):
     return float(np.array([int(h, 16)], dtype=np.uint32).view(np.float32)[0])
 
 
-@pytest.mark.parametrize("case", ["csg32_nested", "csg256_chain", "random_a"])
+@pytest.mark.parametrize("case", ["csg256_chain", "random_a"])
 def test_spatial_groups_enclose_their_primitives(hostonly, case):
     """Spatial collect (scene_jit.c gen_spatial): each wave-level group test's sphere
     (centre and R, R^2 as emitted) encloses the bounding sphere of every primitive the
@@ -487,6 +491,146 @@ def test_spatial_groups_enclose_their_primitives(hostonly, case):
     # every primitive once in the first pass and once in the re-collect pass
     ords_all = [int(x) for x in re.findall(r"// primitive (\d+) ", src)]
     assert sorted(ords_all) == sorted(list(range(nprim)) * 2)
+
+
+def _tree_regions(prog, nrec):
+    """Per CSG node (postfix order) its children, primitive ordinals, bounds box, a
+    sphere around its geometry and its relevance box, restated independently of
+    scene_jit.c's rtree_build: a primitive's box from its sphere members and axis
+    half-spaces, its sphere its smallest sphere member; a union's box the hull and its
+    sphere the enclosing sphere of its operands', an intersection's box the meet and
+    its sphere the smaller operand's, a difference's its left operand's (RDIFF: the
+    right); the relevance box the meet of the boxes of the operands gating the node
+    (an intersection's other operand, a difference's left one for its right one)."""
+    INF = math.inf
+    nodes, st = [], []
+    for pc in range(nrec):
+        r = prog[pc]
+        if r.op == wl.WO_OP_PRIM:
+            lo, hi, sph = [-INF] * 3, [INF] * 3, None
+            for m in range(r.u0):
+                L = prog[pc + 1 + m]
+                if L.op == wl.WO_LEAF_SPHERE:
+                    rr = math.sqrt(L.f[3])
+                    for a in range(3):
+                        lo[a], hi[a] = max(lo[a], L.f[a] - rr), min(hi[a], L.f[a] + rr)
+                    if sph is None or rr < sph[3]:
+                        sph = (L.f[0], L.f[1], L.f[2], rr)
+                elif L.op == wl.WO_LEAF_HALFSPACE and 1 <= L.u1 <= 3:
+                    a = L.u1 - 1
+                    if L.f[a] > 0:
+                        hi[a] = min(hi[a], L.f[3])
+                    else:
+                        lo[a] = max(lo[a], -L.f[3])
+            nodes.append({"op": 0, "ords": [r.u1], "box": (lo, hi), "sph": sph})
+            st.append(len(nodes) - 1)
+        elif r.op in (wl.WO_OP_UNION, wl.WO_OP_INTER, wl.WO_OP_DIFF, wl.WO_OP_RDIFF):
+            b, a = st.pop(), st.pop()
+            A, B = nodes[a], nodes[b]
+            if r.op == wl.WO_OP_UNION:
+                box = ([min(x, y) for x, y in zip(A["box"][0], B["box"][0])],
+                       [max(x, y) for x, y in zip(A["box"][1], B["box"][1])])
+                sph = None
+                if A["sph"] and B["sph"]:
+                    (ca, ra), (cb, rb) = (A["sph"][:3], A["sph"][3]), (B["sph"][:3], B["sph"][3])
+                    d = math.dist(ca, cb)
+                    if d + rb <= ra:
+                        sph = A["sph"]
+                    elif d + ra <= rb:
+                        sph = B["sph"]
+                    else:
+                        R = 0.5 * (d + ra + rb)
+                        sph = tuple(ca[k] + (cb[k] - ca[k]) / d * (R - ra) for k in range(3)) + (R,)
+            elif r.op == wl.WO_OP_INTER:
+                box = ([max(x, y) for x, y in zip(A["box"][0], B["box"][0])],
+                       [min(x, y) for x, y in zip(A["box"][1], B["box"][1])])
+                cand = [x for x in (A["sph"], B["sph"]) if x]
+                sph = min(cand, key=lambda q: q[3]) if cand else None
+            else:
+                keep = A if r.op == wl.WO_OP_DIFF else B
+                box, sph = keep["box"], keep["sph"]
+            nodes.append({"op": r.op, "l": a, "r": b, "ords": A["ords"] + B["ords"], "box": box, "sph": sph})
+            st.append(len(nodes) - 1)
+    root = st[-1]
+    rel = {root: ([-INF] * 3, [INF] * 3)}
+    meet = lambda x, y: ([max(p, q) for p, q in zip(x[0], y[0])], [min(p, q) for p, q in zip(x[1], y[1])])
+    for i in range(len(nodes) - 1, -1, -1):
+        n = nodes[i]
+        if n["op"] == 0:
+            continue
+        c = rel[i]
+        gate_l = n["op"] in (wl.WO_OP_INTER, wl.WO_OP_RDIFF)
+        gate_r = n["op"] in (wl.WO_OP_INTER, wl.WO_OP_DIFF)
+        rel[n["l"]] = meet(c, nodes[n["r"]]["box"]) if gate_l else c
+        rel[n["r"]] = meet(c, nodes[n["l"]]["box"]) if gate_r else c
+    for i, n in enumerate(nodes):
+        n["rel"] = rel[i]
+    return nodes, root
+
+
+@pytest.mark.parametrize("case", ["csg32_nested", "csg360_nested"])
+def test_relevance_groups_enclose_their_subtrees(hostonly, case):
+    """The tree collect of the truth-table forms (scene_jit.c gen_rtree): each wave-level
+    relevance group's sphere (centre and R, R^2 as emitted) encloses a region that holds
+    the subtree's geometry where it is relevant -- the subtree's own sphere, or every
+    corner of the meet of its bounds and relevance box -- so a culled group only ever
+    zeroes bits that cannot change the root; the groups nest as the tree does, every
+    primitive is collected at most once per pass, in the same order in both, and a
+    primitive is left out only where the meet of its bounds and relevance box is empty."""
+    r = wl.Renderer("rg", max_nodes=4096)
+    _build_case(r, case)
+    prog, nrec, nprim = r.program()
+    src = r.jit_source()
+    r.close()
+    nodes, root = _tree_regions(prog, nrec)
+    lines = src.splitlines()
+    end1 = next(i for i, l in enumerate(lines) if 'WO_MARK("collect_end")' in l)
+    first_pass = lines[:end1]
+    # the groups in the order the tree walk emits them: nodes with >= min primitives,
+    # depth first; matched by their primitive lists
+    groups = 0
+    for i, l in enumerate(first_pass):
+        m = re.search(r"// relevance group (\d+) \((\d+) primitives\)", l)
+        if not m:
+            continue
+        groups += 1
+        lits = re.findall(r"0x([0-9a-f]{8})", "\n".join(first_pass[i:i + 12]))
+        r2, cx, cy, cz, rad = (_f32(x) for x in lits[:5])
+        j = next(k for k in range(i, len(first_pass)) if first_pass[k].strip().startswith("if (!(cull["))
+        ind = len(first_pass[j]) - len(first_pass[j].lstrip())
+        k = j + 1
+        while not (first_pass[k].strip() == "}" and len(first_pass[k]) - len(first_pass[k].lstrip()) == ind):
+            k += 1
+        ords = sorted(int(x) for x in re.findall(r"// primitive (\d+) ", "\n".join(first_pass[j:k])))
+        # the node: the subtree with exactly m.group(2) primitives containing these ordinals
+        cands = [n for n in nodes if n["op"] and len(n["ords"]) == int(m.group(2)) and set(ords) <= set(n["ords"])]
+        assert cands, (case, m.group(1), ords)
+        ok = False
+        for n in cands:
+            s_ok = n["sph"] is not None and \
+                math.dist(n["sph"][:3], (cx, cy, cz)) + n["sph"][3] <= rad * (1 + 1e-5)
+            lo = [max(p, q) for p, q in zip(n["box"][0], n["rel"][0])]
+            hi = [min(p, q) for p, q in zip(n["box"][1], n["rel"][1])]
+            b_ok = all(math.isfinite(v) for v in lo + hi) and all(
+                math.dist((x, y, z), (cx, cy, cz)) <= rad * (1 + 1e-5)
+                for x in (lo[0], hi[0]) for y in (lo[1], hi[1]) for z in (lo[2], hi[2]))
+            ok = ok or s_ok or b_ok
+        assert ok, (case, m.group(1), rad)
+        assert rad * rad <= r2 * (1 + 1e-5)
+    assert groups >= 2
+    # every primitive at most once per pass, the same ones in the same order in both passes
+    first = [int(x) for x in re.findall(r"// primitive (\d+) ", "\n".join(first_pass))]
+    second = [int(x) for x in re.findall(r"// primitive (\d+) ", "\n".join(lines[end1:]))]
+    assert len(set(first)) == len(first) and first == second
+    # left out: exactly where the primitive's bounds meet its relevance box in nothing
+    # (the generator's slack may keep a near-empty one; never drop a non-empty one)
+    for n in nodes:
+        if n["op"]:
+            continue
+        lo = [max(p, q) for p, q in zip(n["box"][0], n["rel"][0])]
+        hi = [min(p, q) for p, q in zip(n["box"][1], n["rel"][1])]
+        if n["ords"][0] not in first:
+            assert any(a > b for a, b in zip(lo, hi)), (case, n["ords"][0])
 
 
 @pytest.mark.parametrize("case", ["csg32", "unionpairs_s"])
