@@ -49,13 +49,15 @@ rs)
         "rsc4:400:python tools/root_step.py --scene csg32 --width 3840 --height 2160 --spp 256 --worlds 2 4 8 --map-back bgra > gpurun_out/r05_root_step_c4.log 2>&1"
     ;;
 final)
-    # the round's last build: every bench line, then the headline's, the nested tree's and
-    # csg360's profiles (csg360_nested now takes the specialised kernel)
-    bash "$0" bench || exit $?
+    # the round's last build: the nested tree's, csg360's and the headline's profiles
+    # first (on a fresh box: two sessions that profiled the nested tree after other
+    # scenes' runs measured ~1 GB of writes per launch that no fresh session repeats),
+    # then every bench line
     bash $S \
-        "p32:400:bash tools/profile_session.sh r05f_csg32 --steps 20 --warmup 3" \
-        "p32n:400:bash tools/profile_session.sh r05f_csg32_nested --scene csg32_nested --steps 10 --warmup 2" \
-        "p360:900:bash tools/profile_session.sh r05f_csg360 --scene csg360_nested --steps 3 --warmup 1"
+        "p32n:400:bash tools/profile_session.sh r05h_csg32_nested --scene csg32_nested --steps 10 --warmup 2" \
+        "p360:900:bash tools/profile_session.sh r05h_csg360 --scene csg360_nested --steps 3 --warmup 1" \
+        "p32:400:bash tools/profile_session.sh r05h_csg32 --steps 20 --warmup 3" || exit $?
+    bash "$0" bench
     ;;
 rsnomap)
     # the same without the present map-back (bench.py's N-GPU frame is not presented)
