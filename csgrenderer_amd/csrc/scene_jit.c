@@ -2185,7 +2185,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * at 6 / 7 / 8). */
     /* 14 for the levelled tables' big trees (csg360_nested with the flat evaluation:
      * 250.7 / 243.9 / 235.7 ms at 10 / 12 / 14 events and 5 waves per SIMD, 241.5 at 16
-     * and 4 waves; 304.6 at 5 and 8 waves) */
+     * and 4 waves; 304.6 at 5 and 8 waves; with the tables and relevance groups, 6 waves:
+     * 179.8 ms at 14, 179.2 at 16; 7 waves 179.3; 5 waves 184.5, at 12 events 189.0) */
     bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW %d\n#endif\n", use_lut ? 8 : use_hlut ? 14 : 5);
     if (g.term_mode) bput(&b, "// term mode: %u terms (%u outside the spatial hierarchy)\n", n_jterms, g.ntunb);
     /* small scenes run 8 waves per SIMD: a 7-entry LDS list keeps 8 workgroups'
@@ -2495,7 +2496,7 @@ kernel_tail:
     bput(&b,
          "\n#ifndef WO_JIT_MIN_WAVES\n"
          "#define WO_JIT_MIN_WAVES %u\n#endif\n",
-         n_uterms ? 7u : use_hlut ? 5u : (n_prims > 64u || g.lds_events) ? 8u : 7u);
+         n_uterms ? 7u : use_hlut ? 6u : (n_prims > 64u || g.lds_events) ? 8u : 7u);
     bput(&b,
          "extern \"C\" __global__ __launch_bounds__(256, WO_JIT_MIN_WAVES) void wo_jit_pathtrace(\n"
          "    const WoRec* __restrict__ prog, const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t local_rows,\n"
