@@ -54,9 +54,9 @@ final)
     # scenes' runs measured ~1 GB of writes per launch that no fresh session repeats),
     # then every bench line
     bash $S \
-        "p32n:400:bash tools/profile_session.sh r05h_csg32_nested --scene csg32_nested --steps 10 --warmup 2" \
-        "p360:900:bash tools/profile_session.sh r05h_csg360 --scene csg360_nested --steps 3 --warmup 1" \
-        "p32:400:bash tools/profile_session.sh r05h_csg32 --steps 20 --warmup 3" || exit $?
+        "p32n:400:bash tools/profile_session.sh r05j_csg32_nested --scene csg32_nested --steps 10 --warmup 2" \
+        "p360:900:bash tools/profile_session.sh r05j_csg360 --scene csg360_nested --steps 3 --warmup 1" \
+        "p32:400:bash tools/profile_session.sh r05j_csg32 --steps 20 --warmup 3" || exit $?
     bash "$0" bench
     ;;
 rsnomap)
