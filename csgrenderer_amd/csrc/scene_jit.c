@@ -1910,13 +1910,42 @@ static void gen_rtree_node(Gen* g, int x, int indent) {
         }
         bput(g->b, "%*sif (!(cull[%u] & %uu)) {\n", indent, "", k / 32, 1u << (k % 32));
         inner = indent + 2;
+        if (!g->first_pass) {
+            /* a re-collect wants the events after `after` only: a group whose sphere ends
+             * before that key's t on every lane holds none (its primitives' events lie
+             * inside the sphere; the margin covers the fp32 arithmetic of both) */
+            const float fc[3] = {(float)c[0], (float)c[1], (float)c[2]};
+            const float fRm = (float)(R * (1.0 + 1e-4) + 1e-4);
+            bput(g->b,
+                 "#if WO_RECOLLECT_BEHIND\n"
+                 "%*sfloat ox%u, oy%u, oz%u;\n"
+                 "%*sasm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(ox%u) : \"v\"(o.x));\n"
+                 "%*sasm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oy%u) : \"v\"(o.y));\n"
+                 "%*sasm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(oz%u) : \"v\"(o.z));\n"
+                 "%*sconst float tca%u = __builtin_fmaf(oz%u, d.z, __builtin_fmaf(oy%u, d.y, ox%u * d.x));\n"
+                 "%*sif (__ballot(!(__builtin_fmaf(1e-4f, fabsf(tca%u), tca%u) + __uint_as_float(0x%08xu) < tafter)) != 0ull)\n"
+                 "#endif\n"
+                 "%*s{\n",
+                 inner, "", k, k, k, inner, "", fbits(fc[0]), k, inner, "", fbits(fc[1]), k, inner, "", fbits(fc[2]), k,
+                 inner, "", k, k, k, k, inner, "", k, k, fbits(fRm), inner, "");
+            inner += 2;
+        }
     }
     gen_rtree_node(g, n->l, inner);
     gen_rtree_node(g, n->r, inner);
+    if (test && !g->first_pass) bput(g->b, "%*s}\n", indent + 2, "");
     if (test) bput(g->b, "%*s}\n", indent, "");
 }
 
-static void gen_rtree(Gen* g, int indent) { gen_rtree_node(g, g->rtree->root, indent); }
+static void gen_rtree(Gen* g, int indent) {
+    if (!g->first_pass)
+        bput(g->b,
+             "#ifndef WO_RECOLLECT_BEHIND\n#define WO_RECOLLECT_BEHIND 1\n#endif\n"
+             "%*sconst float tafter = __uint_as_float((uint32_t)(after >> 32));  // the last processed key's t\n"
+             "%*s(void)tafter;\n",
+             indent, "", indent, "");
+    gen_rtree_node(g, g->rtree->root, indent);
+}
 
 char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prims) {
     Buf b = {0};
