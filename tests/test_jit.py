@@ -850,3 +850,26 @@ def test_term_transitions_match_the_sweep(tmp_path):
     bad = lib.run(200000, ctypes.byref(hits))
     assert hits.value > 50000  # the cases hit often enough to mean something
     assert bad == 0, f"{bad} rays differ"
+
+
+@pytest.mark.parametrize("case,want", [("csg360_nested", 1), ("csg256_chain", 0), ("csg256_balanced", 0),
+                                       ("csg32_nested", 0), ("csg32", 0), ("csg512_balanced", 0)])
+def test_levelled_tables_take_only_big_general_trees(hostonly, case, want):
+    """The levelled truth tables (scene_jit.c hlut_plan) are generated for a general tree
+    above lut_plan's 64 primitives whose levels of <= 8 units reach the root within 4
+    (csg360_nested: 62, 10, 2, 1 units); a left-deep chain (too many levels: decision
+    lists), a union of terms (the union count / term mode) and the small trees (one
+    level of tables, or term mode) do not take them.  The renderer routes a general tree
+    above WOLOLO_JIT_MAX_PRIMS to the specialised kernel exactly when they apply."""
+    r = wl.Renderer("hl", max_nodes=4096)
+    scenes.build(case, r)
+    src = r.jit_source()
+    r.close()
+    assert f"#define WO_JIT_HLUT {want}\n" in src, case
+    if want:
+        m = re.search(r"// root by (\d+) levels of truth tables \(units per level:([\d ]+)\)", src)
+        units = [int(x) for x in m.group(2).split()]
+        assert int(m.group(1)) == len(units) <= 4 and units[-1] == 1
+        assert all(a > b for a, b in zip(units, units[1:]))
+        info = re.search(r"kHInfo\[(\d+)\]", src)
+        assert int(info.group(1)) == 309 + sum(units[:-1])  # an entry per lower index per level
