@@ -184,6 +184,7 @@ def main():
         over["spp"] = args.spp
     params = info.params(**over)
     r.set_tracer("interpreter" if args.jit == 0 else args.tracer)
+    r.prepare()  # the kernel AUTO settles on, its background compile included (csg360: the lanes meanwhile)
     W, H, T = params.width, params.height, args.tile_rows
     band = wl.default_band(world) if args.band == "auto" else tuple(int(x) for x in args.band.split(":"))
     args.band_w = band if world > 1 else (0, 0)
@@ -398,6 +399,7 @@ def side_scene(name, args, dev):
     info = scenes.build(name, r)
     params = info.params(max_depth=args.depth)
     r.set_tracer("interpreter" if args.jit == 0 else args.tracer)
+    r.prepare()
     W, H, T = params.width, params.height, args.tile_rows
     out = torch.empty((wl.local_rows(H, T, 1), W, 4), dtype=torch.float32, device=dev)
     seg = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -552,6 +554,7 @@ def single_process(args):
     r.set_tracer("interpreter" if args.jit == 0 else args.tracer)
     if r.set_devices(n) != n or r.device_count() != n:
         fail(f"wo_renderer_set_devices({n}) failed: {wl.last_error()}")
+    r.prepare()
     W, H = params.width, params.height
     frames = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) for _ in range(2)]
     cs = torch.cuda.current_stream(dev)

@@ -515,7 +515,8 @@ static void jit_job_poll(Wo_Renderer* r, int wait) {
     char* src = r->jit_want;
     r->jit_want = NULL;
     if (rc) {
-        fprintf(stderr, WO_LOG_PREFIX " scene specialisation failed (%s); using the interpreter kernel\n", err);
+        fprintf(stderr, WO_LOG_PREFIX " scene specialisation failed (%s); using the %s\n", err,
+                r->lanes_loaded ? "lane tracer" : "interpreter kernel");
     } else if (src && !r->dev_stale) {
         const int cur = r->ndevs > 1 ? wo_dev_current() : -1;
         int ok = 1;
@@ -557,7 +558,9 @@ static int sync_device_ex(Wo_Renderer* r, int may_defer) {
         return -1;
     }
     if (wo_renderer_compile(r) < 0) return -1;
-    if (!r->dev_stale) jit_job_poll(r, !may_defer);
+    /* a batch render waits for a pending compile unless the lanes render meanwhile
+     * (AUTO; an explicit WO_TRACER_JIT asks for the specialised kernel itself) */
+    if (!r->dev_stale) jit_job_poll(r, !may_defer && !(r->lanes_loaded && r->tracer == WO_TRACER_AUTO));
     if (r->dev_stale) {
         jit_job_orphan(r);
         char err[256] = {0};
@@ -620,7 +623,11 @@ static int sync_device_ex(Wo_Renderer* r, int may_defer) {
             pre_src = NULL;
             if (!src) {
                 fprintf(stderr, WO_LOG_PREFIX " scene specialisation: source generation failed; using the interpreter\n");
-            } else if (may_defer && !wo_dev_jit_cached(r->dev, src) && (r->jit_job = wo_jit_job_start(r->dev, src))) {
+            } else if ((may_defer || (lanes_meanwhile && r->tracer == WO_TRACER_AUTO)) && !wo_dev_jit_cached(r->dev, src) &&
+                       (r->jit_job = wo_jit_job_start(r->dev, src))) {
+                /* A batch render of such a scene (AUTO) does not wait for the 1-2 minute
+                 * compile of a big general tree either: the lanes render it meanwhile,
+                 * the same image bit for bit (wo_renderer_prepare waits for the kernel). */
                 r->jit_want = src; /* compiling in the background; the interpreter (or the lanes) meanwhile */
                 src = NULL;
                 deferred = 1;
@@ -633,12 +640,16 @@ static int sync_device_ex(Wo_Renderer* r, int may_defer) {
                 int ok = 1;
                 for (uint32_t i = 0; i < r->ndevs && ok; ++i) {
                     if (wo_dev_set_jit(r->devs[i], src, err, sizeof err) != 0) {
-                        fprintf(stderr, WO_LOG_PREFIX " scene specialisation failed (%s); using the interpreter kernel\n",
-                                err);
+                        fprintf(stderr, WO_LOG_PREFIX " scene specialisation failed (%s); using the %s\n", err,
+                                lanes_meanwhile ? "lane tracer" : "interpreter kernel");
                         ok = 0;
                     }
                 }
                 r->jit_loaded = ok;
+                if (!ok && lanes_meanwhile) { /* the lanes this scene qualified for, not the interpreter */
+                    for (uint32_t i = 0; i < r->ndevs; ++i) wo_dev_set_lanes(r->devs[i], 1);
+                    r->lanes_loaded = 1;
+                }
             }
             free(src);
         }
@@ -651,6 +662,15 @@ static int sync_device_ex(Wo_Renderer* r, int may_defer) {
 }
 
 static int sync_device(Wo_Renderer* r) { return sync_device_ex(r, 0); }
+
+int wo_renderer_prepare(Wo_Renderer* r) {
+    if (!r) return -1;
+    if (sync_device(r)) return -1;
+    const int cur = r->ndevs > 1 ? wo_dev_current() : -1;
+    jit_job_poll(r, 1);
+    if (cur >= 0) (void)wo_dev_select(cur);
+    return 0;
+}
 
 void wo_renderer_set_tracer(Wo_Renderer* r, Wo_Tracer tracer) {
     if (r->tracer != (int)tracer) {

@@ -228,9 +228,9 @@ struct InterpTracer {
         if (nprims > 64u && ((nprims - 64u) & 31u)) hib[((nprims - 64u) >> 5) * 64u + lane] = hib_acc;
 
         // pass 2: sweep events in key order; the first root flip is the hit
-        if (win.k[0] == kEmptyKey) return false;
+        if (win.empty()) return false;
         uint32_t root = st & 1u;
-        while (win.k[0] != kEmptyKey) {
+        while (!win.empty()) {
             uint64_t key = win.pop();
             WO_WK(WO_WORK_SWEEP_STEPS);
             uint32_t ord = key_ord(key);
@@ -241,7 +241,7 @@ struct InterpTracer {
                 return true;
             }
             root = r;
-            if (win.k[0] == kEmptyKey && win.dropped()) {
+            if (win.empty() && win.dropped()) {
                 // window exhausted but events were dropped: re-collect the events
                 // strictly after `key` (the membership state carries on)
                 WO_WK(WO_WORK_RECOLLECTS);

@@ -144,6 +144,7 @@ SIGNATURES = {
     "wo_renderer_trace_path": (c_char_p, [c_void_p]),
     "wo_renderer_set_jit_async": (None, [c_void_p, c_int]),
     "wo_renderer_jit_pending": (c_int, [c_void_p]),
+    "wo_renderer_prepare": (c_int, [c_void_p]),
     "wo_renderer_jit_source": (c_void_p, [c_void_p]),
     "wo_jit_compile_check": (c_int, [c_char_p, c_char_p, c_char_p, c_size_t]),
     "wo_jit_code_object": (ctypes.c_longlong, [c_char_p, c_char_p, POINTER(c_int), POINTER(c_double), c_char_p,
@@ -335,6 +336,12 @@ class Renderer:
 
     def jit_pending(self) -> bool:
         return bool(self.lib.wo_renderer_jit_pending(self.ptr))
+
+    def prepare(self):
+        """Compile, upload and load the scene's kernels now, waiting for a background
+        compile (renderer_ext.h wo_renderer_prepare)."""
+        if self.lib.wo_renderer_prepare(self.ptr) != 0:
+            raise WololoError(last_error())
 
     def trace_path(self) -> str:
         return self.lib.wo_renderer_trace_path(self.ptr).decode()

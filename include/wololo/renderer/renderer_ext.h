@@ -239,11 +239,18 @@ char const* wo_renderer_trace_path(Wo_Renderer* r);
  * renders with the interpreter -- the same image bit for bit -- until the compile
  * has ended; the first draw_frame after that switches to it.  render_f32,
  * render_accumulate, render_rows_device, render_frame_device and count_work wait
- * for a compile in flight (batch renders get the specialised kernel).  The
+ * for a compile in flight (batch renders get the specialised kernel) -- except
+ * under WO_TRACER_AUTO for a general tree above 256 primitives (1-2 minutes of
+ * hiprtc), which the lane tracer renders meanwhile in batch renders too.  The
  * nodes are added incrementally as in the reference (renderer.c:2232-2275). */
 void wo_renderer_set_jit_async(Wo_Renderer* r, int on);
 /* 1 while a background compile of the current scene's kernel is in flight. */
 int wo_renderer_jit_pending(Wo_Renderer* r);
+/* Compile, upload and load the current scene's kernels now, waiting for any
+ * background compile (a benchmark's set-up: the timed frames then run the
+ * kernel AUTO settles on).  Extends the reference's per-frame scene upload
+ * (renderer.c:2085-2219 records it into every frame); 0, or -1 on failure. */
+int wo_renderer_prepare(Wo_Renderer* r);
 
 /* HIP source of the scene-specialised kernel for the current scene (NULL if
  * the scene has no primitives); release with wo_free(). */

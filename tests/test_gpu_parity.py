@@ -7,6 +7,7 @@ failure message shows which bar broke.
 """
 import json
 import os
+import time
 
 import numpy as np
 import pytest
@@ -565,6 +566,12 @@ def test_auto_tracer_choices(monkeypatch):
             monkeypatch.setenv("WOLOLO_JIT_GENERAL", "0")  # the lanes' general form instead
         r, info = _scene(name, "auto")
         r.render(info.params(width=32, height=18, spp=1))
+        if name == "csg360_nested" and want == "jit":
+            # a batch render does not wait for the big tree's compile (the lanes meanwhile,
+            # test_big_general_tree_renders_on_the_lanes_while_it_compiles); prepare() does
+            assert r.trace_path() in ("jit", "lanes"), r.trace_path()
+            r.prepare()
+            r.render(info.params(width=32, height=18, spp=1))
         assert r.trace_path() == want, (name, r.trace_path())
         if name == "rtiow_cover":
             assert r.lanes_info()["kind"] == 3, r.lanes_info()  # kLanesBvhSpheres: the binary walk
@@ -577,6 +584,33 @@ def test_auto_tracer_choices(monkeypatch):
         if name == "csg360_nested" and want == "lanes":
             assert r.lanes_info()["kind"] == 7, r.lanes_info()  # kLanesGeneral
         r.close()
+
+
+@pytest.mark.timeout(600)
+def test_big_general_tree_renders_on_the_lanes_while_it_compiles(monkeypatch):
+    """a batch render (render_f32) of a general tree above 256 primitives under
+    AUTO used to compile its specialised kernel inline (1-2 minutes of hiprtc for
+    csg360_nested).  With the code object in neither cache it now starts the compile in
+    the background and renders on the lane tracer meanwhile -- the same image bit for
+    bit -- and prepare() waits for the kernel and loads it."""
+    # a flag no other test uses: the code object is in neither cache
+    monkeypatch.setenv("WOLOLO_JIT_FLAGS", f"-DWO_TEST_NONCE={os.getpid()}")
+    r, info = _scene("csg360_nested", "auto")
+    p = info.params(width=48, height=27, spp=2, seed=3)
+    t0 = time.perf_counter()
+    img0 = r.render(p)
+    dt = time.perf_counter() - t0
+    assert r.trace_path() == "lanes" and r.jit_pending(), (r.trace_path(), r.jit_pending())
+    img1 = r.render(p)  # another batch render: still no wait while the lanes are loaded
+    r.prepare()
+    assert not r.jit_pending()
+    img2 = r.render(p)
+    assert r.trace_path() == "jit", r.trace_path()
+    assert np.array_equal(img0, img1) and np.array_equal(img0, img2)
+    ref, _ = _oracle_rows(r, p)
+    _cmp(img2, ref, "csg360_nested after prepare")
+    print(f"first batch render on the lanes: {dt:.2f} s")
+    r.close()
 
 
 @pytest.mark.parametrize("window", ["lds2", "default"])
