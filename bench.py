@@ -144,7 +144,13 @@ def main():
     if world > 1 and args.hw_queues > 0:
         # before the first HIP call of this process (tools/root_step.py, N = 8, rank 0's
         # step: csg32 0.385 -> 0.355 ms, csg32_nested 1.116 -> 0.945 ms with 8 queues)
-        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 16))
+        # an explicit setting from the caller wins (and the line records the value used)
+        if "GPU_MAX_HW_QUEUES" in os.environ:
+            if os.environ["GPU_MAX_HW_QUEUES"] != str(min(args.hw_queues, 16)):
+                print(f"[bench] GPU_MAX_HW_QUEUES={os.environ['GPU_MAX_HW_QUEUES']} from the environment "
+                      f"(not --hw-queues {args.hw_queues})", file=sys.stderr)
+        else:
+            os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 16))
     import torch
     import torch.distributed as dist
 
@@ -461,6 +467,9 @@ def report_line(args, r, info, params, world, elapsed_s, segs_all, segs_local, k
                                                                                           "pathtrace_kernel"),
                 "kernel_ms": round(k_ms, 4), "segments_per_launch": segs_local // steps,
                 "trace_path": r.trace_path(),
+                # the code object the timed launches ran (its key and resources), so a
+                # profile or a traffic figure can be matched to it
+                "kernel_object": r.kernel_info(),
                 "brute_force_flop_per_segment": info.flop_per_segment,
                 "brute_force_achieved": round(brute_tf, 3),
                 "brute_force_frac": round(brute_tf / PEAK_FP32_TFLOPS, 4)}
@@ -495,7 +504,18 @@ def report_line(args, r, info, params, world, elapsed_s, segs_all, segs_local, k
             pmc = json.load(open(args.pmc_json))
             key = f"{args.scene}:{W}x{H}:{params.spp}:{world}:{roof.get('trace_path', 'ubershader')}"
             if key in pmc:
-                roof["traffic"] = pmc[key]
+                ent = pmc[key]
+                if isinstance(ent, dict):
+                    # recorded with the profiled kernel's key: used only for the same code object
+                    ko = roof.get("kernel_object") or {}
+                    if ent.get("kernel_key") == ko.get("key"):
+                        roof["traffic"] = ent["bytes"]
+                        roof["traffic_kernel_key_match"] = True
+                    else:
+                        roof["traffic_kernel_key_match"] = False
+                        roof["traffic_recorded_for"] = ent.get("kernel_key")
+                else:
+                    roof["traffic"] = ent  # a round-5 figure, recorded without a kernel key
         except Exception as e:  # report, don't fail the bench
             print(f"[bench] pmc json unreadable: {e}", file=sys.stderr)
     cpu = None

@@ -700,6 +700,11 @@ int wo_renderer_lanes_info(Wo_Renderer* r, uint32_t* out) {
     return wo_dev_lanes_info(r->dev, out);
 }
 
+int wo_renderer_kernel_info(Wo_Renderer* r, char* key_hex, uint32_t* out) {
+    if (!r || !r->dev || !out) return -1;
+    return wo_dev_kernel_info(r->dev, key_hex, out);
+}
+
 char const* wo_renderer_trace_path(Wo_Renderer* r) {
     if (!r->dev) return "none";
     return r->jit_loaded ? "jit" : r->lanes_loaded ? "lanes" : "interpreter";

@@ -1484,16 +1484,20 @@ static void hplan_free(HPlan* h) {
     memset(h, 0, sizeof *h);
 }
 
-/* units below x at the current level (unit_of[y] >= 0: y roots lower unit unit_of[y]) */
-static uint32_t h_count(const TNode* t, int x, const int* unit_of, uint32_t* cnt, uint32_t* first) {
+/* units below x at the current level (unit_of[y] >= 0: y roots lower unit unit_of[y]);
+ * *gap is set when the two operands' units are not adjacent ranges (a unit's table
+ * is indexed by the contiguous range [first, first + cnt) of the lower level) */
+static uint32_t h_count(const TNode* t, int x, const int* unit_of, uint32_t* cnt, uint32_t* first, int* gap) {
     if (unit_of[x] >= 0) {
         cnt[x] = 1u;
         first[x] = (uint32_t)unit_of[x];
         return 1u;
     }
-    const uint32_t a = h_count(t, t[x].l, unit_of, cnt, first), b = h_count(t, t[x].r, unit_of, cnt, first);
+    const int l = t[x].l, r = t[x].r;
+    const uint32_t a = h_count(t, l, unit_of, cnt, first, gap), b = h_count(t, r, unit_of, cnt, first, gap);
     cnt[x] = a + b;
-    first[x] = first[t[x].l] < first[t[x].r] ? first[t[x].l] : first[t[x].r];
+    first[x] = first[l] < first[r] ? first[l] : first[r];
+    if (first[l] + cnt[l] != first[r] && first[r] + cnt[r] != first[l]) *gap = 1;
     return a + b;
 }
 
@@ -1551,10 +1555,14 @@ static int hlut_plan(const WoRec* prog, uint32_t n_recs, uint32_t n_prims, HPlan
         if (!ok) break;
         const int b = st[--sp], a = st[--sp];
         TNode x = {(int)r->op, a, b, t[a].lo < t[b].lo ? t[a].lo : t[b].lo, t[a].n + t[b].n};
+        /* the operands' primitives must be adjacent ranges of ordinals, as lut_plan
+         * requires (the scene compiler numbers them in postfix order); another
+         * numbering falls back to the decision lists or the lanes */
+        ok = t[a].lo + t[a].n == t[b].lo || t[b].lo + t[b].n == t[a].lo;
         t[nt] = x;
         st[sp++] = (int)nt++;
     }
-    ok = ok && sp == 1u && t[st[0]].n == n_prims;
+    ok = ok && sp == 1u && t[st[0]].lo == 0u && t[st[0]].n == n_prims;
     const int root = ok ? st[0] : 0;
     /* level 0's units: the primitives (their ordinals) */
     for (uint32_t x = 0; ok && x < nt; ++x) unit_of[x] = t[x].op == 0 ? (int)t[x].lo : -1;
@@ -1565,7 +1573,12 @@ static int hlut_plan(const WoRec* prog, uint32_t n_recs, uint32_t n_prims, HPlan
             break;
         }
         const uint32_t L = h->L;
-        h_count(t, root, unit_of, cnt, first);
+        int gap = 0;
+        h_count(t, root, unit_of, cnt, first, &gap);
+        if (gap) {
+            ok = 0;
+            break;
+        }
         uint32_t k = 0;
         h_split(t, root, cnt, first, roots, &k);
         ok = k >= 1u && k <= 255u;
@@ -1932,8 +1945,14 @@ static void gen_rtree_node(Gen* g, int x, int indent) {
         }
         if (!g->first_pass) {
             /* a re-collect wants the events after `after` only: a group whose sphere ends
-             * before that key's t on every lane holds none (its primitives' events lie
-             * inside the sphere; the margin covers the fp32 arithmetic of both) */
+             * before that key's t on every lane cannot change the root any more.  A ray
+             * that has left a sphere never re-enters it (convex), and outside the group's
+             * sphere the subtree is empty or gated off -- the first pass's cull argument,
+             * which covers half-spaces and a sphere drawn around the meet of the subtree's
+             * bounds with its relevance box alike (the primitives' events need not lie
+             * inside it).  So the primitives' bits may stay at their values at `after`.
+             * The margin covers the fp32 arithmetic; tests/test_jit.py::
+             * test_recollect_behind_skip_keeps_the_root restates it in float64. */
             const float fc[3] = {(float)c[0], (float)c[1], (float)c[2]};
             const float fRm = (float)(R * (1.0 + 1e-4) + 1e-4);
             bput(g->b,

@@ -1356,6 +1356,10 @@ extern "C" int wo_fastmath_check(int which, uint32_t lo_bits, uint32_t hi_bits, 
 // ===========================================================================
 // Host glue (C ABI declared in wo_dev.h)
 // ===========================================================================
+// big tiles per resident workgroup of a rank's share (plan_tiles), every kernel;
+// a generated source may name its own (`// wo_share_tiles N`, scene_jit.c)
+constexpr uint32_t kShareTiles = 3u;
+
 struct WoDev {
     int device;
     int cus;           // compute units (multiProcessorCount)
@@ -2629,7 +2633,7 @@ extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t err
     {
         const char* m = strstr(src, "// wo_share_tiles ");
         const int v = m ? atoi(m + strlen("// wo_share_tiles ")) : 0;
-        dev->jit_share_tiles = v >= 1 && v <= 64 ? (uint32_t)v : 8u;
+        dev->jit_share_tiles = v >= 1 && v <= 64 ? (uint32_t)v : kShareTiles;
     }
     dev->jit_origin = origin;
     dev->jit_compile_sec = sec;
@@ -2759,7 +2763,8 @@ static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, u
     if (big) {
         tail_rounds = 0.0;
     } else {
-        // The largest shape that gives every resident workgroup >= 8 tiles: a
+        // The largest shape that gives every resident workgroup >= want_per_wg tiles
+        // (kShareTiles = 3 for every kernel since round 5, see the end of this note): a
         // workgroup's tiles then average out the costly ones (glass, deep CSG),
         // which otherwise set the end of a short launch.  8x8 keeps a 3-round
         // tail of 4x4 tiles, 8x4 a 2-round one.  Measured (tools/rank_share.py,
@@ -2783,6 +2788,8 @@ static PathLaunch plan_tiles(uint32_t width, uint32_t rows, uint32_t resident, u
         // every scene (want 3 / 8, N = 8 projection): csg32 6.86 / 6.40x, csg32_nested
         // 7.67 / 7.27x, balanced 7.17 / 6.78x, chain 6.99 / 6.88x, RTIOW 7.37 / 6.97x,
         // csg512 6.00 / 5.45x, C4 7.59 / 7.60x (profiles/r05_root_step_want_hwq8.log).
+        // So every kernel passes kShareTiles (the lane tracer, the interpreter and a
+        // specialised kernel without the generator's marker included).
         const char* tw = getenv("WOLOLO_TILE_WANT");  // (measurement) tiles per resident workgroup
         const char* ts = getenv("WOLOLO_TILE_SPAN");  // (measurement) 8x8 tiles may span two row bands
         const uint64_t want_tiles = (uint64_t)(tw && *tw ? (uint32_t)atoi(tw) : want_per_wg) * resident;
@@ -2839,6 +2846,53 @@ static hipError_t static_occupancy(PathKind kind, size_t dyn_lds, int* per_cu) {
     default:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, pathtrace_kernel<false, kCount>, kBlock, dyn_lds);
     }
+}
+
+// Resources of one path kernel as the runtime loaded it (hipFuncGetAttributes):
+// private (scratch) bytes per lane, VGPRs, static LDS.
+template <bool kCount>
+static hipError_t static_attrs(PathKind kind, hipFuncAttributes* a) {
+    switch (kind) {
+    case kLanesBvh: return hipFuncGetAttributes(a, (const void*)pathtrace_lanes_kernel<2, kCount>);
+    case kLanesBvhSpheres: return hipFuncGetAttributes(a, (const void*)pathtrace_lanes_kernel<3, kCount>);
+    case kLanesTerms: return hipFuncGetAttributes(a, (const void*)pathtrace_lanes_kernel<6, kCount>);
+    case kLanesGeneral: return hipFuncGetAttributes(a, (const void*)pathtrace_lanes_kernel<7, kCount>);
+    case kLanesDynWideTerms: return hipFuncGetAttributes(a, (const void*)pathtrace_lanes_kernel<14, kCount>);
+    case kInterpLds: return hipFuncGetAttributes(a, (const void*)pathtrace_kernel<true, kCount>);
+    default: return hipFuncGetAttributes(a, (const void*)pathtrace_kernel<false, kCount>);
+    }
+}
+
+// The path kernel of the last launch: key_hex (65 bytes) gets the specialised
+// kernel's code-object key (jit_key) or "static:<kind>"; out[0] = kind (PathKind),
+// out[1] = private bytes per lane, out[2] = registers (VGPRs), out[3] = static LDS
+// bytes.  A profile session records these beside its counters, so a summary says
+// which code object it measured.
+extern "C" int wo_dev_kernel_info(WoDev* dev, char* key_hex, uint32_t* out) {
+    if (!dev || !out || dev->last_kind == 0u) return -1;
+    const PathKind kind = (PathKind)dev->last_kind;
+    if (hipSetDevice(dev->device) != hipSuccess) return -1;
+    out[0] = (uint32_t)kind;
+    if (kind == kJit) {
+        if (!dev->jit_fn) return -1;
+        int local = 0, regs = 0, lds = 0;
+        if (hipFuncGetAttribute(&local, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, dev->jit_fn) != hipSuccess ||
+            hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, dev->jit_fn) != hipSuccess ||
+            hipFuncGetAttribute(&lds, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, dev->jit_fn) != hipSuccess)
+            return -1;
+        out[1] = (uint32_t)local;
+        out[2] = (uint32_t)regs;
+        out[3] = (uint32_t)lds;
+        if (key_hex) snprintf(key_hex, 65, "%s", dev->jit_key.c_str());
+    } else {
+        hipFuncAttributes a;
+        if (static_attrs<false>(kind, &a) != hipSuccess) return -1;
+        out[1] = (uint32_t)a.localSizeBytes;
+        out[2] = (uint32_t)a.numRegs;
+        out[3] = (uint32_t)a.sharedSizeBytes;
+        if (key_hex) snprintf(key_hex, 65, "static:%u", (unsigned)kind);
+    }
+    return 0;
 }
 
 template <int kMode, bool kCount>
@@ -2986,7 +3040,7 @@ static int launch_impl(WoDev* dev, WoFrame const* frame_in, void* d_out, void* s
         // a rank's local rows are bands of tile_rows consecutive frame rows: a tile
         // taller than a band would join rows far apart (incoherent primary rays)
         PathLaunch tg = plan_tiles(fr.width, local_rows, (uint32_t)dev->cus * (uint32_t)per_cu,
-                                   fr.nranks > 1u ? fr.tile_rows : ~0u, kind == kJit ? dev->jit_share_tiles : 3u);
+                                   fr.nranks > 1u ? fr.tile_rows : ~0u, kind == kJit ? dev->jit_share_tiles : kShareTiles);
         if (d_accum && fr.mode == WO_MODE_PATHTRACE) {
             tg.acc = d_accum;
             tg.acc_spp = accum_spp;

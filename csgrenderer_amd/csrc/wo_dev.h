@@ -136,6 +136,8 @@ int wo_jit_disk_store(const char* key_hex, const void* code, size_t size);
  * device's specialised kernel was loaded from. */
 int wo_dev_jit_origin(WoDev* dev, double* seconds);
 int wo_dev_lanes_info(WoDev* dev, uint32_t* out);
+/* the last launch's path kernel: key (65 B), out[4] = kind, scratch B/lane, VGPRs, LDS */
+int wo_dev_kernel_info(WoDev* dev, char* key_hex, uint32_t* out);
 /* Wait for the slot's frame; *host = its pixels (RGBA float; NULL when the
  * submit did not map them back), *host_bgra8 (if non-NULL) = its present
  * encode; both valid until the slot is submitted again. */

@@ -151,6 +151,7 @@ SIGNATURES = {
                                                c_char_p, c_size_t]),
     "wo_renderer_jit_info": (c_int, [c_void_p, POINTER(c_double)]),
     "wo_renderer_lanes_info": (c_int, [c_void_p, POINTER(c_uint32)]),
+    "wo_renderer_kernel_info": (c_int, [c_void_p, c_char_p, POINTER(c_uint32)]),
     "wo_free": (None, [c_void_p]),
     "wo_renderer_node_count": (c_size_t, [c_void_p]),
     "wo_renderer_name": (c_char_p, [c_void_p]),
@@ -336,6 +337,16 @@ class Renderer:
 
     def jit_pending(self) -> bool:
         return bool(self.lib.wo_renderer_jit_pending(self.ptr))
+
+    def kernel_info(self):
+        """The last launch's path kernel as loaded (renderer_ext.h wo_renderer_kernel_info):
+        {"key", "kind", "scratch_bytes", "vgprs", "lds_bytes"}, or None before a path launch."""
+        key = ctypes.create_string_buffer(65)
+        out = (c_uint32 * 4)()
+        if self.lib.wo_renderer_kernel_info(self.ptr, key, out) != 0:
+            return None
+        return {"key": key.value.decode(), "kind": int(out[0]), "scratch_bytes": int(out[1]),
+                "vgprs": int(out[2]), "lds_bytes": int(out[3])}
 
     def prepare(self):
         """Compile, upload and load the scene's kernels now, waiting for a background

@@ -278,6 +278,12 @@ int wo_renderer_jit_info(Wo_Renderer* r, double* seconds);
  * forms, 11-14 the resumable walk; trace_kernels.hip PathKind).  `out` holds 5
  * entries.  Returns 0, or -1 when the renderer does not run the lane tracer. */
 int wo_renderer_lanes_info(Wo_Renderer* r, uint32_t* out);
+/* The path kernel of the last launch as the runtime loaded it: key_hex (65 bytes)
+ * gets the specialised kernel's code-object key (SHA-256 of source, options and
+ * toolchain) or "static:<kind>"; out[0] = kind (as lanes_info's), out[1] = private
+ * (scratch) bytes per lane, out[2] = VGPRs, out[3] = static LDS bytes.  Profile
+ * sessions record it beside their counters.  0, or -1 before any path launch. */
+int wo_renderer_kernel_info(Wo_Renderer* r, char* key_hex, uint32_t* out);
 void wo_free(void* p);
 
 size_t wo_renderer_node_count(Wo_Renderer* r);

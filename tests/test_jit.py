@@ -873,3 +873,92 @@ def test_levelled_tables_take_only_big_general_trees(hostonly, case, want):
         assert all(a > b for a, b in zip(units, units[1:]))
         info = re.search(r"kHInfo\[(\d+)\]", src)
         assert int(info.group(1)) == 309 + sum(units[:-1])  # an entry per lower index per level
+
+
+def _prim_bits(prog, nrec, P):
+    """Membership of every primitive at points P (n, 3), float64 from the fp32 records,
+    as words of bits (n x words, uint32) for _program_value."""
+    P = np.asarray(P, dtype=np.float64)
+    nprim = sum(1 for i in range(nrec) if prog[i].op == wl.WO_OP_PRIM)
+    bits = np.zeros((len(P), (nprim + 31) // 32), dtype=np.uint32)
+    pc = 0
+    while pc < nrec:
+        rec = prog[pc]
+        if rec.op != wl.WO_OP_PRIM:
+            pc += 1
+            continue
+        v = np.ones(len(P), dtype=bool)
+        for m in range(rec.u0):
+            L = prog[pc + 1 + m]
+            f = np.array(L.f[:4], dtype=np.float64)
+            v &= (((P - f[:3]) ** 2).sum(axis=1) <= f[3]) if L.op == wl.WO_LEAF_SPHERE else (P @ f[:3] <= f[3])
+        bits[:, rec.u1 // 32] |= v.astype(np.uint32) << np.uint32(rec.u1 % 32)
+        pc += 1 + rec.u0
+    return bits
+
+
+@pytest.mark.parametrize("case", ["csg32_nested", "csg360_nested"])
+def test_recollect_behind_skip_keeps_the_root(hostonly, case):
+    """the re-collect pass (WO_RECOLLECT_BEHIND) skips a relevance group whose
+    sphere ends, on every lane, before the last processed key's t.  The skip is exact
+    because a ray that has left a sphere never re-enters it (a sphere is convex) and,
+    outside the group's sphere, the group's subtree is empty or gated off -- the first
+    pass's cull argument, which holds for half-spaces and for a sphere drawn around the
+    meet of the subtree's bounds with its relevance box alike.  Restated here: along
+    random unit rays, with the skipped groups' primitives frozen at their membership
+    at t_after (what the kernel's bits hold then), the root equals the true root at
+    every sampled t > t_after.  Group spheres and margins are read from the emitted
+    re-collect pass; membership in float64 from the fp32 records."""
+    r = wl.Renderer("rb", max_nodes=4096)
+    _build_case(r, case)
+    prog, nrec, nprim = r.program()
+    src = r.jit_source()
+    r.close()
+    lines = src.splitlines()
+    end1 = next(i for i, l in enumerate(lines) if 'WO_MARK("collect_end")' in l)
+    second = lines[end1:]
+    groups = []  # (centre, margin literal, ordinals inside)
+    for i, l in enumerate(second):
+        if l.strip() != "#if WO_RECOLLECT_BEHIND":
+            continue
+        lits = re.findall(r"0x([0-9a-f]{8})", "\n".join(second[i + 1:i + 7]))
+        c = np.array([_f32(x) for x in lits[:3]], dtype=np.float64)
+        marg = _f32(lits[3])
+        j = next(k for k in range(i, len(second)) if second[k].strip() == "#endif") + 1
+        assert second[j].strip() == "{"
+        ind = len(second[j]) - len(second[j].lstrip())
+        k = j + 1
+        while not (second[k].strip() == "}" and len(second[k]) - len(second[k].lstrip()) == ind):
+            k += 1
+        ords = [int(x) for x in re.findall(r"// primitive (\d+) ", "\n".join(second[j:k]))]
+        groups.append((c, marg, ords))
+    assert len(groups) >= 2, case
+    rng = np.random.default_rng(11)
+    lo = np.array([-6.0, -2.0, -6.0])
+    hi = np.array([6.0, 6.0, 6.0])
+    nray, nt = 600, 160
+    skipped_any = 0
+    for _ in range(nray):
+        o = rng.uniform(lo, hi)
+        d = rng.normal(size=3)
+        d /= np.linalg.norm(d)
+        ta = float(rng.uniform(0.01, 12.0))
+        skip = set()
+        for c, marg, ords in groups:
+            tca = float((c - o) @ d)
+            if tca + 1e-4 * abs(tca) + marg < ta:
+                skip.update(ords)
+        if not skip:
+            continue
+        skipped_any += 1
+        ts = ta + np.sort(rng.uniform(0.0, 30.0, nt))
+        P = o[None, :] + ts[:, None] * d[None, :]
+        true_bits = _prim_bits(prog, nrec, P)
+        frozen0 = _prim_bits(prog, nrec, (o + ta * d)[None, :])[0]
+        mask = np.zeros(true_bits.shape[1], dtype=np.uint32)
+        for p in skip:
+            mask[p // 32] |= np.uint32(1) << np.uint32(p % 32)
+        frozen = (true_bits & ~mask) | (frozen0 & mask)
+        assert np.array_equal(_program_value(prog, nrec, true_bits), _program_value(prog, nrec, frozen)), \
+            (case, o, d, ta, sorted(skip))
+    assert skipped_any >= nray // 10, (case, skipped_any)

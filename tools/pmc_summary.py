@@ -63,6 +63,27 @@ def main():
         if a.timed and len(durs) >= a.timed:
             res["timed_dispatches"] = a.timed
             res["timed_avg_ms"] = sum(durs[-a.timed:]) / a.timed
+    # which code object each pass ran: the bench line's roofline.kernel_object (key,
+    # scratch bytes per lane, VGPRs) from every pass's log; the passes must agree, and
+    # the kernel trace's Scratch_Size is recorded beside it
+    objs = {}
+    for name in ("kstats", "fetch", "write", "pmc1", "pmc2"):
+        lg = os.path.join(a.dir, name + ".log")
+        if not os.path.exists(lg):
+            continue
+        for line in open(lg, errors="replace"):
+            line = line.strip()
+            if line.startswith("{") and '"roofline"' in line:
+                try:
+                    objs[name] = json.loads(line)["roofline"].get("kernel_object")
+                except ValueError:
+                    pass
+    keys = {json.dumps(v, sort_keys=True) for v in objs.values()}
+    res["kernel_object"] = next(iter(objs.values()), None)
+    res["kernel_object_passes"] = sorted(objs)
+    res["kernel_object_consistent"] = len(keys) == 1
+    scr = sorted({r["Scratch_Size"] for r in trows if any(k in r["Kernel_Name"] for k in KERNELS)})
+    res["trace_scratch_size"] = [int(x) for x in scr]
     ffiles, f = counters(a.dir, "fetch")
     wfiles, w = counters(a.dir, "write")
     p1files, p1 = counters(a.dir, "pmc1")
@@ -84,9 +105,14 @@ def main():
         res["clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / (res["avg_ms"] * 1e-3) / 1e9
     json.dump(res, sys.stdout, indent=1)
     print()
+    if not res["kernel_object_consistent"]:
+        print("ERROR: the passes ran different code objects: " + json.dumps(objs), file=sys.stderr)
+        return 2
     if a.save and a.key and "traffic_bytes" in res:
         j = json.load(open(a.save)) if os.path.exists(a.save) else {}
-        j[a.key] = res["traffic_bytes"]
+        ko = res.get("kernel_object") or {}
+        j[a.key] = {"bytes": res["traffic_bytes"], "kernel_key": ko.get("key"),
+                    "scratch_bytes": ko.get("scratch_bytes")}
         json.dump(j, open(a.save, "w"), indent=1)
         print(f"recorded {a.key} = {res['traffic_bytes']} in {a.save}")
     if a.copy:
@@ -96,7 +122,8 @@ def main():
             for i, fn in enumerate(files[:1]):
                 shutil.copy(fn, os.path.join(root, "profiles", f"{a.copy}_{tag}.csv"))
         json.dump(res, open(os.path.join(root, "profiles", f"{a.copy}_summary.json"), "w"), indent=1)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

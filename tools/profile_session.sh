@@ -19,7 +19,11 @@ run() {
     timeout -k 10 300 rocprofv3 "$@" -d "$out/$name" -o "$name" --output-format csv -- \
         python3 bench.py --no-cpu-baseline --no-count-work --no-draw-frame --side-scenes "" "${BENCH_ARGS[@]}" > "$out/$name.log" 2>&1
     local rc=$?
-    echo "[$tag/$name] rc=$rc"
+    # the code object this pass ran (key, scratch bytes per lane, VGPRs): the summary
+    # checks that every pass ran the same one
+    echo "[$tag/$name] rc=$rc kernel_object=$(python3 -c 'import json,sys
+for l in open(sys.argv[1], errors="replace"):
+    if l.startswith("{") and "\"roofline\"" in l: print(json.dumps(json.loads(l)["roofline"].get("kernel_object")))' "$out/$name.log" 2>/dev/null)"
     return $rc
 }
 BENCH_ARGS=("$@")
