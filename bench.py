@@ -144,13 +144,15 @@ def main():
     if world > 1 and args.hw_queues > 0:
         # before the first HIP call of this process (tools/root_step.py, N = 8, rank 0's
         # step: csg32 0.385 -> 0.355 ms, csg32_nested 1.116 -> 0.945 ms with 8 queues)
-        # an explicit setting from the caller wins (and the line records the value used)
-        if "GPU_MAX_HW_QUEUES" in os.environ:
-            if os.environ["GPU_MAX_HW_QUEUES"] != str(min(args.hw_queues, 16)):
-                print(f"[bench] GPU_MAX_HW_QUEUES={os.environ['GPU_MAX_HW_QUEUES']} from the environment "
-                      f"(not --hw-queues {args.hw_queues})", file=sys.stderr)
-        else:
-            os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 16))
+        # --hw-queues 0 leaves the environment's value alone; otherwise an inherited
+        # value is replaced, and said so (the GPU box exports HIP's default, 4; the
+        # line records the value used in config.hw_queues)
+        want = str(min(args.hw_queues, 16))
+        had = os.environ.get("GPU_MAX_HW_QUEUES")
+        if had is not None and had != want:
+            print(f"[bench] GPU_MAX_HW_QUEUES={had} from the environment replaced by {want} "
+                  f"(--hw-queues; 0 keeps it)", file=sys.stderr)
+        os.environ["GPU_MAX_HW_QUEUES"] = want
     import torch
     import torch.distributed as dist
 
@@ -679,8 +681,8 @@ def cpu_baseline(r, params, budget_s: float):
         row = (row + n) % params.height
     dt = time.perf_counter() - t0
     return {"value": round(segs / dt / 1e6, 4), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
-            "host_cpus": pyoracle.host_cpus(),
-            "threads_from": "OMP_NUM_THREADS" if os.environ.get("OMP_NUM_THREADS") else "affinity mask",
+            "host_cpus": pyoracle.host_cpus(), "cpu_quota": pyoracle.cpu_quota(),
+            "threads_from": pyoracle.threads_source(),
             "sample": f"{rows} of {params.height} rows (from row {start}, wrapping) of the "
                       f"same {params.width}x{params.height} frame, {params.spp} spp, {params.max_depth} bounces; "
                       f"{segs} segments in {dt:.1f} s"}

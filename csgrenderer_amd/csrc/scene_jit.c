@@ -245,15 +245,15 @@ static void gen_collect(Gen* g, uint32_t start, uint32_t end, int indent) {
             if (g->first_pass)
                 bput(g->b,
                      "%*s    bits[%u] |= ((iv.a <= tmin) & (iv.b > tmin) ? 1u : 0u) << %u;\n"
-                     "%*s    if (iv.a > tmin) { WO_WK(WO_WORK_EVENTS); win.insert(wodev::event_key_lo(iv.a, ka | iv.ma)); }\n"
-                     "%*s    if ((iv.b > tmin) & (iv.b < wodev::kInf)) { WO_WK(WO_WORK_EVENTS); win.insert(wodev::event_key_lo(iv.b, kb | iv.mb)); }\n"
+                     "%*s    { const bool c = iv.a > tmin; WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, wodev::event_key_lo(iv.a, ka | iv.ma)); }\n"
+                     "%*s    { const bool c = (iv.b > tmin) & (iv.b < wodev::kInf); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, wodev::event_key_lo(iv.b, kb | iv.mb)); }\n"
                      "%*s  }\n%*s}\n",
                      indent, "", ord / 32, ord % 32, indent, "", indent, "", indent, "", indent, "");
             else
                 bput(g->b,
                      "%*s    uint64_t k0 = wodev::event_key_lo(iv.a, ka | iv.ma), k1 = wodev::event_key_lo(iv.b, kb | iv.mb);\n"
-                     "%*s    if ((iv.a > tmin) & (k0 > after)) { WO_WK(WO_WORK_EVENTS); win.insert(k0); }\n"
-                     "%*s    if ((iv.b > tmin) & (iv.b < wodev::kInf) & (k1 > after)) { WO_WK(WO_WORK_EVENTS); win.insert(k1); }\n"
+                     "%*s    { const bool c = (iv.a > tmin) & (k0 > after); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, k0); }\n"
+                     "%*s    { const bool c = (iv.b > tmin) & (iv.b < wodev::kInf) & (k1 > after); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, k1); }\n"
                      "%*s  }\n%*s}\n",
                      indent, "", indent, "", indent, "", indent, "", indent, "");
             pc += 1 + cnt;
@@ -290,14 +290,14 @@ static void gen_lone_sphere(Gen* g, const WoRec* L, uint32_t ord, int indent) {
     if (g->first_pass)
         bput(g->b,
              "%*s      bits[%u] |= ((la <= tmin) & (lb > tmin) ? 1u : 0u) << %u;\n"
-             "%*s      if (la > tmin) { WO_WK(WO_WORK_EVENTS); win.insert(wodev::event_key_lo(la, ka)); }\n"
-             "%*s      if ((lb > tmin) & (lb < wodev::kInf)) { WO_WK(WO_WORK_EVENTS); win.insert(wodev::event_key_lo(lb, kb)); }\n",
+             "%*s      { const bool c = la > tmin; WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, wodev::event_key_lo(la, ka)); }\n"
+             "%*s      { const bool c = (lb > tmin) & (lb < wodev::kInf); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, wodev::event_key_lo(lb, kb)); }\n",
              indent, "", ord / 32, ord % 32, indent, "", indent, "");
     else
         bput(g->b,
              "%*s      const uint64_t k0 = wodev::event_key_lo(la, ka), k1 = wodev::event_key_lo(lb, kb);\n"
-             "%*s      if ((la > tmin) & (k0 > after)) { WO_WK(WO_WORK_EVENTS); win.insert(k0); }\n"
-             "%*s      if ((lb > tmin) & (lb < wodev::kInf) & (k1 > after)) { WO_WK(WO_WORK_EVENTS); win.insert(k1); }\n",
+             "%*s      { const bool c = (la > tmin) & (k0 > after); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, k0); }\n"
+             "%*s      { const bool c = (lb > tmin) & (lb < wodev::kInf) & (k1 > after); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, k1); }\n",
              indent, "", indent, "", indent, "");
     bput(g->b, "%*s    }\n%*s  }\n%*s}\n", indent, "", indent, "", indent, "");
 }
@@ -2360,7 +2360,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             bput(&b,
                  "    // the smallest term transition after `after` (its rise flag in the key)\n"
                  "    // and the number of terms true at t_min\n"
-                 "    uint64_t best = wodev::kEmptyKey, after = 0ull;\n"
+                 "    uint64_t best = wodev::kBestNone, after = 0ull;\n"
                  "    uint32_t cnt = 0u;\n"
                  "    (void)after;\n"
                  "    WO_MARK(\"collect_begin\");\n"
@@ -2371,7 +2371,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  "    }\n"
                  "    WO_MARK(\"collect_end\");\n"
                  "    WO_TMARK();\n"
-                 "    if (best == wodev::kEmptyKey) return false;\n"
+                 "    if (best == wodev::kBestNone) return false;\n"
                  "    const bool root = cnt != 0u;\n"
                  "    for (;;) {\n"
                  "      WO_WK(WO_WORK_SWEEP_STEPS);\n"
@@ -2383,14 +2383,14 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  "      }\n"
                  "      // the count moved without flipping the root: the next transition\n"
                  "      after = best;\n"
-                 "      best = wodev::kEmptyKey;\n"
+                 "      best = wodev::kBestNone;\n"
                  "      WO_WK(WO_WORK_RECOLLECTS);\n"
                  "      {\n");
             g.first_pass = 0;
             gen_collect_all(&g, 8);
             bput(&b,
                  "      }\n"
-                 "      if (best == wodev::kEmptyKey) return false;\n"
+                 "      if (best == wodev::kBestNone) return false;\n"
                  "    }\n"
                  "  }\n"
                  "};\n");

@@ -55,13 +55,47 @@ def host_cpus() -> int:
         return max(1, os.cpu_count() or 1)
 
 
-def nthreads_default() -> int:
-    """OMP_NUM_THREADS when set (the GPU box sets it to the job's CPU share), else
-    every CPU of the affinity mask."""
+def cpu_quota():
+    """The cgroup's CPU bandwidth limit in CPUs (cgroup v2 cpu.max, or v1
+    cfs_quota_us / cfs_period_us), rounded up; None when unlimited or unknown."""
+    import math
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, math.ceil(int(q) / int(per)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return max(1, math.ceil(q / per)) if q > 0 and per > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
+def usable_cpus() -> int:
+    """The CPUs this process can use at once: the affinity mask, capped by the
+    cgroup's CPU quota (the GPU box: 256 CPUs in the mask, a 16-CPU quota -- more
+    threads than the quota only time-share it)."""
+    n, q = host_cpus(), cpu_quota()
+    return min(n, q) if q else n
+
+
+def threads_source() -> str:
     n = os.environ.get("OMP_NUM_THREADS")
-    if n and n.isdigit():
+    if n and n.isdigit() and int(n) != usable_cpus():
+        return "OMP_NUM_THREADS override"
+    return "affinity mask capped by the cgroup CPU quota" if cpu_quota() else "affinity mask"
+
+
+def nthreads_default() -> int:
+    """Every usable CPU (usable_cpus); OMP_NUM_THREADS only as an explicit override
+    that differs from it (threads_source names which applied)."""
+    n = os.environ.get("OMP_NUM_THREADS")
+    if n and n.isdigit() and int(n) != usable_cpus():
         return max(1, int(n))
-    return host_cpus()
+    return usable_cpus()
 
 
 def ubershader_pixel(x, y, w, h, t, mode=0):

@@ -711,6 +711,18 @@ inline uint64_t event_key_lo(float t, uint32_t lo) {
     memcpy(&u, &t, 4);
     return ((uint64_t)u << 32) | lo;
 }
+// the device's v_min_f64 on keys as doubles (IEEE minNum: a quiet NaN operand gives
+// the other operand, bits unchanged)
+#define WO_WIN_F64 1
+inline uint64_t key_min(uint64_t a, uint64_t b) {
+    double x, y;
+    memcpy(&x, &a, 8);
+    memcpy(&y, &b, 8);
+    const double r = std::fmin(x, y);
+    uint64_t u;
+    memcpy(&u, &r, 8);
+    return u;
+}
 @TERM@
 }  // namespace wodev
 using namespace wodev;
@@ -777,19 +789,19 @@ static void term_pass(const std::vector<Ivl>& iv, const std::vector<Term>& terms
 }
 
 static bool term_method(const std::vector<Ivl>& iv, const std::vector<Term>& terms, uint64_t& key, bool& after_val) {
-    uint64_t best = kEmptyKey;
+    uint64_t best = kBestNone;
     uint32_t cnt = 0;
     term_pass<true>(iv, terms, 0ull, best, cnt);
-    if (best == kEmptyKey) return false;
+    if (best == kBestNone) return false;
     const bool root = cnt != 0u;
     for (;;) {
         cnt = term_rises(best) ? cnt + 1u : cnt - 1u;
         if ((cnt != 0u) != root) { key = term_event(best); after_val = cnt != 0u; return true; }
         const uint64_t after = best;
-        best = kEmptyKey;
+        best = kBestNone;
         uint32_t unused = 0;
         term_pass<false>(iv, terms, after, best, unused);
-        if (best == kEmptyKey) return false;
+        if (best == kBestNone) return false;
     }
 }
 
