@@ -725,10 +725,8 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
         if (first) bput(g->b, "%*s  cnt += %swodev::term_in0(x) ? 1u : 0u;\n", indent, "", pos[0] ? "" : "!");
         bput(g->b,
              "%*s  WO_WK(WO_WORK_EVENTS);\n"
-             "%*s  wodev::term_cand(x.kin, x.valid & (x.kin != 0ull)%s, best);\n"
-             "%*s  wodev::term_cand(x.kout, x.valid & (x.kout != wodev::kEmptyKey)%s, best);\n%*s}\n",
-             indent, "", indent, "", first ? "" : " & (x.kin > after)", indent, "",
-             first ? "" : " & (x.kout > after)", indent, "");
+             "%*s  wodev::term_cands1<%s>(x, after, best);\n%*s}\n",
+             indent, "", indent, "", first ? "true" : "false", indent, "");
         return;
     }
     const uint32_t o1 = g->prog[pcs[1]].u1;
@@ -750,11 +748,12 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
              pos[0] ? "" : "!", pos[1] ? "" : "!");
     bput(g->b,
          "%*s    WO_WK(WO_WORK_EVENTS);\n"
-         "%*s    wodev::term_cands_of<%s, %s>(x, y, after, best);\n"
-         "%*s    wodev::term_cands_of<%s, %s>(y, x, after, best);\n"
+         "%*s    wodev::term_cands_of<%s, %s, %s>(x, y, after, best);\n"
+         "%*s    wodev::term_cands_of<%s, %s, %s>(y, x, after, best);\n"
          "%*s  }\n%*s}\n",
-         indent, "", indent, "", pos[1] ? "true" : "false", first ? "true" : "false", indent, "",
-         pos[0] ? "true" : "false", first ? "true" : "false", indent, "", indent, "");
+         indent, "", indent, "", pos[1] ? "true" : "false", first ? "true" : "false", o1 < o0 ? "true" : "false",
+         indent, "", pos[0] ? "true" : "false", first ? "true" : "false", o0 < o1 ? "true" : "false", indent, "",
+         indent, "");
 }
 
 /* ---- eval, flattened: literal sets as one masked compare ----

@@ -772,8 +772,7 @@ static void term_pass(const std::vector<Ivl>& iv, const std::vector<Term>& terms
         const TermLit x = term_lit(iv[o0], term_ka(o0, t.pos[0]), term_kb(o0, t.pos[0]));
         if (t.n == 1) {
             if (kFirst) cnt += (t.pos[0] ? term_in0(x) : !term_in0(x)) ? 1u : 0u;
-            term_cand(x.kin, x.valid & (x.kin != 0ull) & (kFirst | (x.kin > after)), best);
-            term_cand(x.kout, x.valid & (x.kout != kEmptyKey) & (kFirst | (x.kout > after)), best);
+            term_cands1<kFirst>(x, after, best);
             continue;
         }
         if (t.pos[0] && !x.valid) continue;  // the wave-level skip, per lane
@@ -781,10 +780,18 @@ static void term_pass(const std::vector<Ivl>& iv, const std::vector<Term>& terms
         const TermLit y = term_lit(iv[o1], term_ka(o1, t.pos[1]), term_kb(o1, t.pos[1]));
         if (kFirst)
             cnt += ((t.pos[0] ? term_in0(x) : !term_in0(x)) & (t.pos[1] ? term_in0(y) : !term_in0(y))) ? 1u : 0u;
-        if (t.pos[1]) term_cands_of<true, kFirst>(x, y, after, best);
-        else term_cands_of<false, kFirst>(x, y, after, best);
-        if (t.pos[0]) term_cands_of<true, kFirst>(y, x, after, best);
-        else term_cands_of<false, kFirst>(y, x, after, best);
+        // kYFirst: the other literal's ordinal is the smaller (the generator's constant)
+        if (o1 < o0) {
+            if (t.pos[1]) term_cands_of<true, kFirst, true>(x, y, after, best);
+            else term_cands_of<false, kFirst, true>(x, y, after, best);
+            if (t.pos[0]) term_cands_of<true, kFirst, false>(y, x, after, best);
+            else term_cands_of<false, kFirst, false>(y, x, after, best);
+        } else {
+            if (t.pos[1]) term_cands_of<true, kFirst, false>(x, y, after, best);
+            else term_cands_of<false, kFirst, false>(x, y, after, best);
+            if (t.pos[0]) term_cands_of<true, kFirst, true>(y, x, after, best);
+            else term_cands_of<false, kFirst, true>(y, x, after, best);
+        }
     }
 }
 
