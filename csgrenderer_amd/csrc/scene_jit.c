@@ -2259,6 +2259,10 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * and 4 waves; 304.6 at 5 and 8 waves; with the tables and relevance groups, 6 waves:
      * 179.8 ms at 14, 179.2 at 16; 7 waves 179.3; 5 waves 184.5, at 12 events 189.0) */
     bput(&b, "#ifndef WO_WINDOW\n#define WO_WINDOW %d\n#endif\n", use_lut ? 8 : use_hlut ? 14 : 5);
+    /* two swept events per trip of the sweep loop (the second without a re-collect):
+     * off -- the second copy's registers spill (csg32_nested 6.78 -> 6.91 ms, chain
+     * 10.06 -> 10.16; profiles/r06_ab_sweep_unroll.txt) */
+    bput(&b, "#ifndef WO_SWEEP_UNROLL\n#define WO_SWEEP_UNROLL 0\n#endif\n");
     if (g.term_mode) bput(&b, "// term mode: %u terms (%u outside the spatial hierarchy)\n", n_jterms, g.ntunb);
     /* small scenes run 8 waves per SIMD: a 7-entry LDS list keeps 8 workgroups'
      * LDS within the CU (csg32 5.24 -> 5.19 ms; csg256 balanced keeps 8 entries:
@@ -2493,6 +2497,23 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             bput(&b,
                  "      }\n"
                  "      // WO_TOGGLE_END\n"
+                 "#if WO_SWEEP_UNROLL\n"
+                 "      // a second event per trip while the window holds one (no re-collect here:\n"
+                 "      // a lane whose window is empty goes round to the top)\n"
+                 "      if (!win.empty()) {\n"
+                 "        if (r != root) { wodev::hit_from_key(key, r, hit); return true; }\n"
+                 "        root = r;\n"
+                 "        win.next(key);\n"
+                 "        WO_WK(WO_WORK_SWEEP_STEPS);\n"
+                 "        {\n"
+                 "          uint32_t ord = ((uint32_t)key) >> 12;\n"
+                 "          uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n");
+            for (uint32_t w = 0; w < nw; ++w) bput(&b, "          bits[%u] ^= w == %uu ? m : 0u;\n", w, w);
+            hlut_emit_update(&b, &hl, nw, 10);
+            bput(&b,
+                 "        }\n"
+                 "      }\n"
+                 "#endif\n"
                  "    }\n"
                  "  }\n"
                  "};\n");
@@ -2551,6 +2572,36 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             bput(&b,
                  "      }\n"
                  "      // WO_TOGGLE_END\n"
+                 "#if WO_SWEEP_UNROLL\n"
+                 "      // a second event per trip while the window holds one (no re-collect here:\n"
+                 "      // a lane whose window is empty goes round to the top)\n"
+                 "      if (!win.empty()) {\n"
+                 "        uint32_t r;\n"
+                 "%s        {\n", use_lut ? "#if WO_JIT_LUT\n" : "");
+            if (use_lut) {
+                lut_emit_eval(&b, &lut, 10);
+                bput(&b, "        }\n#else\n        {\n");
+            }
+            {
+                g.nbound = 0;
+                Term rt = gen_eval_flat(&g, 0, n_recs, 10);
+                uint32_t rv = term_name(&g, &rt, 10);
+                bput(&b, "          r = v%u ? 1u : 0u;\n        }\n", rv);
+            }
+            if (use_lut) bput(&b, "#endif\n");
+            bput(&b,
+                 "        if (r != root) { wodev::hit_from_key(key, r, hit); return true; }\n"
+                 "        root = r;\n"
+                 "        win.next(key);\n"
+                 "        WO_WK(WO_WORK_SWEEP_STEPS);\n"
+                 "        {\n"
+                 "          uint32_t ord = ((uint32_t)key) >> 12;\n"
+                 "          uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n");
+            for (uint32_t w = 0; w < nw; ++w) bput(&b, "          bits[%u] ^= w == %uu ? m : 0u;\n", w, w);
+            bput(&b,
+                 "        }\n"
+                 "      }\n"
+                 "#endif\n"
                  "    }\n"
                  "  }\n"
                  "};\n");
