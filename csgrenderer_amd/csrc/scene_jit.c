@@ -1665,12 +1665,20 @@ static void hlut_emit_update(Buf* b, const HPlan* h, uint32_t nw, int indent) {
         if (nwl == 1u) {
             bput(b, "%*s  const uint32_t idx = (%s[0] >> lo) & ((1u << n) - 1u);\n", indent, "", lowv);
         } else {
-            bput(b, "%*s  const uint32_t w = lo >> 5;\n%*s  uint32_t a0 = %s[0], a1 = %s[1];\n", indent, "", indent, "",
-                 lowv, lowv);
+            bput(b, "%*s  const uint32_t w = lo >> 5;\n", indent, "");
+            /* level 0 with the words in LDS: two reads at the word index (the extra word
+             * past the last is 0) instead of a select per word */
+            /* (at the last word, a1 is any word: a unit's bits never pass the last
+             * primitive, so the shift and mask below take none of a1's) */
+            if (!L)
+                bput(b, "#if WO_HBITS_LDS\n%*s  const uint32_t a0 = bits[w], a1 = bits[w + 1u < %uu ? w + 1u : w];\n#else\n",
+                     indent, "", nwl);
+            bput(b, "%*s  uint32_t a0 = %s[0], a1 = %s[1];\n", indent, "", lowv, lowv);
             for (uint32_t k = 1; k < nwl; ++k) {
                 bput(b, "%*s  a0 = w == %uu ? %s[%u] : a0;\n", indent, "", k, lowv, k);
                 if (k + 1u < nwl) bput(b, "%*s  a1 = w == %uu ? %s[%u] : a1;\n", indent, "", k, lowv, k + 1u);
             }
+            if (!L) bput(b, "#endif\n");
             bput(b, "%*s  const uint32_t idx = (uint32_t)((((uint64_t)a1 << 32) | a0) >> (lo & 31u)) & ((1u << n) - 1u);\n",
                  indent, "");
         }
@@ -2263,6 +2271,15 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * off -- the second copy's registers spill (csg32_nested 6.78 -> 6.91 ms, chain
      * 10.06 -> 10.16; profiles/r06_ab_sweep_unroll.txt) */
     bput(&b, "#ifndef WO_SWEEP_UNROLL\n#define WO_SWEEP_UNROLL 0\n#endif\n");
+    /* the levelled tables' membership words in LDS (wodev::LdsBits) from 4 words; with
+     * them csg360_nested's kernel fits 5 waves per SIMD without scratch (the window of
+     * 14 keys; 130.2 ms, against 131.6 at 6 waves with 60 B of scratch per lane and
+     * 174-178 ms in round 5; windows 16 / 20 at 5 waves: 125.1 / 120.0 ms but 44 / 72 B
+     * of scratch -- the path state spilled around every trace, GBs per frame;
+     * profiles/r06_ab_csg360_lds_bits.txt) */
+    if (use_hlut)
+        bput(&b, "#ifndef WO_HBITS_LDS\n#define WO_HBITS_LDS %d\n#endif\n#define WO_HBITS_WORDS %uu\n",
+             (n_prims + 31u) / 32u >= 4u ? 1 : 0, (n_prims + 31u) / 32u);
     if (g.term_mode) bput(&b, "// term mode: %u terms (%u outside the spatial hierarchy)\n", n_jterms, g.ntunb);
     /* small scenes run 8 waves per SIMD: a 7-entry LDS list keeps 8 workgroups'
      * LDS within the CU (csg32 5.24 -> 5.19 ms; csg256 balanced keeps 8 entries:
@@ -2340,6 +2357,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
          "  const __attribute__((address_space(3))) uint32_t* htab;\n"
          "#define WO_HINFO hinfo\n"
          "#define WO_HTAB htab\n"
+         "#if WO_HBITS_LDS\n"
+         "  wodev::LdsBits::P sbits;  // this lane's column of the membership words (LDS)\n"
+         "#endif\n"
          "#endif\n"
          "  __device__ __forceinline__ WoRec hit_leaf(const wodev::Hit& h) const {\n"
          "    return prog[ordpc[h.ord()] + 1u + h.member()];\n"
@@ -2400,7 +2420,11 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             eval_ops = 4;
             goto kernel_tail;
         }
-        bput(&b, "    uint32_t bits[%u];\n", nw);
+        if (use_hlut)
+            bput(&b, "#if WO_HBITS_LDS\n    wodev::LdsBits bits;\n    bits.p = sbits;\n#else\n    uint32_t bits[%u];\n#endif\n",
+                 nw);
+        else
+            bput(&b, "    uint32_t bits[%u];\n", nw);
         for (uint32_t w = 0; w < nw; ++w) bput(&b, "    bits[%u] = 0u;\n", w);
         bput(&b, "    uint32_t cull[%u];  // bit k: BOUND k culled for this wave\n", ncw);
         for (uint32_t w = 0; w < ncw; ++w) bput(&b, "    cull[%u] = 0u;\n", w);
@@ -2447,10 +2471,11 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  "      const uint32_t ord = ((uint32_t)key) >> 12;\n"
                  "      const uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n"
                  "      uint32_t single = 0u;\n");
-            for (uint32_t w = 0; w < nw; ++w) {
-                bput(&b, "      bits[%u] ^= w == %uu ? m : 0u;\n", w, w);
+            if (use_hlut) bput(&b, "#if WO_HBITS_LDS\n      bits[w] ^= m;\n#else\n");
+            for (uint32_t w = 0; w < nw; ++w) bput(&b, "      bits[%u] ^= w == %uu ? m : 0u;\n", w, w);
+            if (use_hlut) bput(&b, "#endif\n");
+            for (uint32_t w = 0; w < nw; ++w)
                 if (sr[w]) bput(&b, "      single |= w == %uu ? (0x%08xu & m) : 0u;\n", w, sr[w]);
-            }
             bput(&b,
                  "      if (single != 0u) { wodev::hit_from_key(key, 1u, hit); return true; }\n"
                  "      have = true;  // root stays 0\n"
@@ -2492,7 +2517,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  "      {\n"
                  "        uint32_t ord = ((uint32_t)key) >> 12;\n"
                  "        uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n");
+            bput(&b, "#if WO_HBITS_LDS\n        bits[w] ^= m;\n#else\n");
             for (uint32_t w = 0; w < nw; ++w) bput(&b, "        bits[%u] ^= w == %uu ? m : 0u;\n", w, w);
+            bput(&b, "#endif\n");
             hlut_emit_update(&b, &hl, nw, 8);
             bput(&b,
                  "      }\n"
@@ -2508,7 +2535,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  "        {\n"
                  "          uint32_t ord = ((uint32_t)key) >> 12;\n"
                  "          uint32_t w = ord >> 5, m = 1u << (ord & 31u);\n");
+            bput(&b, "#if WO_HBITS_LDS\n          bits[w] ^= m;\n#else\n");
             for (uint32_t w = 0; w < nw; ++w) bput(&b, "          bits[%u] ^= w == %uu ? m : 0u;\n", w, w);
+            bput(&b, "#endif\n");
             hlut_emit_update(&b, &hl, nw, 10);
             bput(&b,
                  "        }\n"
@@ -2618,7 +2647,7 @@ kernel_tail:
     bput(&b,
          "\n#ifndef WO_JIT_MIN_WAVES\n"
          "#define WO_JIT_MIN_WAVES %u\n#endif\n",
-         n_uterms ? 7u : use_hlut ? 6u : (n_prims > 64u || g.lds_events) ? 8u : 7u);
+         n_uterms ? 7u : use_hlut ? ((n_prims + 31u) / 32u >= 4u ? 5u : 6u) : (n_prims > 64u || g.lds_events) ? 8u : 7u);
     bput(&b,
          "extern \"C\" __global__ __launch_bounds__(256, WO_JIT_MIN_WAVES) void wo_jit_pathtrace(\n"
          "    const WoRec* __restrict__ prog, const WoMaterial* __restrict__ mats, WoFrame fr, uint32_t local_rows,\n"
@@ -2641,6 +2670,10 @@ kernel_tail:
          "  for (uint32_t i = threadIdx.x; i < sizeof(kHTab) / 4; i += wodev::kBlock) s_htab[i] = kHTab[i];\n"
          "  tr.hinfo = (const __attribute__((address_space(3))) uint32_t*)s_hinfo;\n"
          "  tr.htab = (const __attribute__((address_space(3))) uint32_t*)s_htab;\n"
+         "#if WO_HBITS_LDS\n"
+         "  __shared__ uint32_t s_bits[WO_HBITS_WORDS * wodev::kBlock];  // the membership words\n"
+         "  tr.sbits = (wodev::LdsBits::P)(s_bits + threadIdx.x);\n"
+         "#endif\n"
          "#endif\n"
          "#if WO_JIT_LDS_PROG  // hit-leaf and material reads from LDS (pathtrace_block's first barrier orders the copy)\n"
          "  __shared__ WoRec s_prog[%u];\n"

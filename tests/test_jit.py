@@ -322,7 +322,7 @@ def _union_of_pairs(r, n, seed):
     return items[0]
 
 
-def _compile_sweep(tmp_path, src, nw, ncull, lut=1):
+def _compile_sweep(tmp_path, src, nw, ncull, lut=1, hbits=1):
     """The generated evaluation and toggle blocks (and the union-count table, or the
     truth tables with WO_JIT_LUT=`lut`) as a host function: evaluate at the start
     membership, then apply toggles, writing the root after each."""
@@ -345,12 +345,13 @@ def _compile_sweep(tmp_path, src, nw, ncull, lut=1):
         m = re.search(r"__constant__ uint32_t " + name + r"\[\d+\] = \{.*?\};", src, re.S)
         if m:
             table += m.group(0).replace("__constant__", "static const") + f"\n#define {macro} {name}\n"
-    table = f"#define WO_JIT_LUT {lut}\n" + table
+    # the levelled tables' words: the LDS form's code (wodev::LdsBits) on a host array
+    table = f"#define WO_JIT_LUT {lut}\n#define WO_HBITS_LDS {hbits}\n" + table
     # the levelled tables' unit values persist from the evaluation into the toggles
     m = re.search(r"^(.*)// WO_STATE_DECL", src, re.M)
     state = m.group(1) + "\n" if m else ""
     root_after = "(ucnt != 0)" if "kUTerm" in table else "r" if "kHTab" in table else None
-    c = tmp_path / f"ev{lut}.cpp"
+    c = tmp_path / f"ev{lut}{hbits}.cpp"
     c.write_text("#include <stddef.h>\n#include <stdint.h>\n" + table +
                  "extern \"C\" void run(const uint32_t* all, int n, const uint32_t* ords, int nev, uint32_t* out) {\n"
                  f"  for (int i = 0; i < n; ++i) {{\n    uint32_t bits[{nw}];\n"
@@ -362,7 +363,7 @@ def _compile_sweep(tmp_path, src, nw, ncull, lut=1):
                  "      const uint64_t key = (uint64_t)ords[(size_t)i * nev + e] << 12;\n" + toggle +
                  ("      out[(size_t)i * (nev + 1) + e + 1] = " + (root_after or "0") + ";\n") +
                  "    }\n  }\n}\n")
-    so = tmp_path / f"ev{lut}.so"
+    so = tmp_path / f"ev{lut}{hbits}.so"
     subprocess.run(["g++", "-O1", "-shared", "-fPIC", "-o", str(so), str(c)], check=True)
     lib = ctypes.CDLL(str(so))
     return lib, root_after is not None
@@ -397,15 +398,17 @@ def test_generated_root_evaluation(hostonly, tmp_path, case):
     if case == "csg360_nested":
         assert "kHTab" in src  # 309 primitives: levels of truth tables, updated per event
     for lut in ((1, 0) if "kLut" in src else (1,)):
-        _check_generated_eval(tmp_path, src, prog, nrec, nprim, lut)
+        # the levelled tables' membership words: the LDS form (wodev::LdsBits) and registers
+        for hbits in ((1, 0) if "WO_HBITS_LDS" in src else (1,)):
+            _check_generated_eval(tmp_path, src, prog, nrec, nprim, lut, hbits)
 
 
-def _check_generated_eval(tmp_path, src, prog, nrec, nprim, lut):
+def _check_generated_eval(tmp_path, src, prog, nrec, nprim, lut, hbits=1):
     import ctypes
 
     nw = (nprim + 31) // 32
     ncull = max(1, len(re.findall(r"cull\[(\d+)\] = 0u;", src)))
-    lib, counted = _compile_sweep(tmp_path, src, nw, ncull, lut)
+    lib, counted = _compile_sweep(tmp_path, src, nw, ncull, lut, hbits)
     rng = np.random.default_rng(7)
     rows = [np.eye(nprim, dtype=np.uint8), np.zeros((1, nprim), dtype=np.uint8)]  # every primitive alone
     for p in (0.01, 0.03, 0.1, 0.3, 0.5):
