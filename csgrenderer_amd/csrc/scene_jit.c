@@ -1997,6 +1997,24 @@ static void gen_rtree(Gen* g, int indent) {
     gen_rtree_node(g, g->rtree->root, indent);
 }
 
+/* The root's value from bits[] (the truth tables, or the flattened evaluation with
+ * WO_JIT_LUT=0) into `out`, as a block of its own (the batch sweep's copies). */
+static void gen_eval_block(Gen* g, const LutPlan* lut, int use_lut, uint32_t n_recs, int indent, const char* out) {
+    bput(g->b, "%*s{\n%*s  uint32_t r;\n%s", indent, "", indent, "", use_lut ? "#if WO_JIT_LUT\n" : "");
+    if (use_lut) {
+        bput(g->b, "%*s  {\n", indent, "");
+        lut_emit_eval(g->b, lut, indent + 4);
+        bput(g->b, "%*s  }\n#else\n", indent, "");
+    }
+    bput(g->b, "%*s  {\n", indent, "");
+    g->nbound = 0;
+    Term rt = gen_eval_flat(g, 0, n_recs, indent + 4);
+    uint32_t rv = term_name(g, &rt, indent + 4);
+    bput(g->b, "%*s    r = v%u ? 1u : 0u;\n%*s  }\n", indent, "", rv, indent, "");
+    if (use_lut) bput(g->b, "#endif\n");
+    bput(g->b, "%*s  %s = r;\n%*s}\n", indent, "", out, indent, "");
+}
+
 char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prims) {
     Buf b = {0};
     Gen g;
@@ -2271,6 +2289,7 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * off -- the second copy's registers spill (csg32_nested 6.78 -> 6.91 ms, chain
      * 10.06 -> 10.16; profiles/r06_ab_sweep_unroll.txt) */
     bput(&b, "#ifndef WO_SWEEP_UNROLL\n#define WO_SWEEP_UNROLL 0\n#endif\n");
+    bput(&b, "#ifndef WO_SWEEP_BATCH\n#define WO_SWEEP_BATCH 1\n#endif\n#ifndef WO_SWEEP_BATCH_EXIT\n#define WO_SWEEP_BATCH_EXIT 1\n#endif\n");
     /* the levelled tables' membership words in LDS (wodev::LdsBits) from 4 words; with
      * them csg360_nested's kernel fits 5 waves per SIMD without scratch (the window of
      * 14 keys; 130.2 ms, against 131.6 at 6 waves with 60 B of scratch per lane and
@@ -2551,6 +2570,64 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             eval_ops = 0;
             for (uint32_t L = 0; L < hl.L; ++L) eval_ops += 12u + 2u * ((L ? (hl.k[L - 1] + 31u) / 32u : nw) - 1u);
         } else {
+            if (nw == 1u) {
+                /* Batch sweep (round 6, WO_SWEEP_BATCH): the root after each of the
+                 * window's events in one straight pass -- the prefix states of the
+                 * membership word (one XOR each) and their evaluations, which do not
+                 * depend on one another -- and the first event whose root differs
+                 * from the root at t_min is the hit.  The event loop ran a trip per
+                 * event, each waiting on the last one's evaluation, for as many trips
+                 * as the wave's slowest lane needed; here every lane does the same
+                 * fixed work per window fill.  Same hit key and value as the loop. */
+                bput(&b, "#if WO_SWEEP_BATCH && !WO_JIT_LDS_EVENTS\n    {\n      uint32_t r0;\n");
+                gen_eval_block(&g, &lut, use_lut, n_recs, 6, "r0");
+                bput(&b,
+                     "      if (have & (r0 != root)) { wodev::hit_from_key(key, r0, hit); return true; }\n"
+                     "      root = r0;\n"
+                     "      uint64_t last = key;  // the last processed event (the first-event block's, or none)\n"
+                     "      for (;;) {\n"
+                     "        uint32_t bb = bits[0], hr = 0u;\n"
+                     "        uint64_t hk = 0ull;\n"
+                     "        bool found = false;\n"
+                     "#pragma unroll\n"
+                     "        for (int j = 0; j < wodev::kWindow; ++j) {\n"
+                     "          const uint64_t kj = win.k[j];\n"
+                     "          const bool v = kj != wodev::Window::kEmpty;\n"
+                     "#if WO_SWEEP_BATCH_EXIT\n"
+                     "          // the window is sorted: no lane has a later event to take once none has this one\n"
+                     "          if (__ballot(v & !found) == 0ull) break;\n"
+                     "#endif\n"
+                     "          bb ^= v ? (1u << ((((uint32_t)kj) >> 12) & 31u)) : 0u;\n"
+                     "          uint32_t rj;\n"
+                     "          {\n"
+                     "            const uint32_t bits[1] = {bb};\n");
+                gen_eval_block(&g, &lut, use_lut, n_recs, 12, "rj");
+                bput(&b,
+                     "          }\n"
+                     "          WO_WK_IF(v & !found, WO_WORK_SWEEP_STEPS);\n"
+                     "          const bool f = v & !found & (rj != root);\n"
+                     "          last = v ? kj : last;\n"
+                     "          hk = f ? kj : hk;\n"
+                     "          hr = f ? rj : hr;\n"
+                     "          found = found | f;\n"
+                     "        }\n"
+                     "        WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);\n"
+                     "        if (found) { wodev::hit_from_key(hk, hr, hit); return true; }\n"
+                     "        bits[0] = bb;\n"
+                     "        if (!win.dropped()) return false;\n"
+                     "        after = last;\n"
+                     "        WO_WK(WO_WORK_RECOLLECTS);\n"
+                     "        win.clear();\n"
+                     "        {\n");
+                g.first_pass = 0;
+                gen_collect_all(&g, 10);
+                bput(&b,
+                     "        }\n"
+                     "        if (win.empty()) return false;\n"
+                     "      }\n"
+                     "    }\n"
+                     "#else\n");
+            }
             bput(&b,
                  "    for (;;) {\n"
                  "      uint32_t r;\n");
@@ -2631,7 +2708,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                  "        }\n"
                  "      }\n"
                  "#endif\n"
-                 "    }\n"
+                 "    }\n");
+            if (nw == 1u) bput(&b, "#endif  // WO_SWEEP_BATCH\n");
+            bput(&b,
                  "  }\n"
                  "};\n");
         }
