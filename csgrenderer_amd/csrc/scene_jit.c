@@ -2570,6 +2570,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
             eval_ops = 0;
             for (uint32_t L = 0; L < hl.L; ++L) eval_ops += 12u + 2u * ((L ? (hl.k[L - 1] + 31u) / 32u : nw) - 1u);
         } else {
+            /* (one membership word: the form above also compiles for up to four, but the
+             * csg256 chain -- four words, a window of 5 -- measured the same 10.06 ms
+             * with it as without; profiles/r06_ab_sweep_batch.txt) */
             if (nw == 1u) {
                 /* Batch sweep (round 6, WO_SWEEP_BATCH): the root after each of the
                  * window's events in one straight pass -- the prefix states of the
@@ -2586,7 +2589,8 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                      "      root = r0;\n"
                      "      uint64_t last = key;  // the last processed event (the first-event block's, or none)\n"
                      "      for (;;) {\n"
-                     "        uint32_t bb = bits[0], hr = 0u;\n"
+                     "        uint32_t bb[%u], hr = 0u;\n"
+                     "        for (int w = 0; w < %u; ++w) bb[w] = bits[w];\n"
                      "        uint64_t hk = 0ull;\n"
                      "        bool found = false;\n"
                      "#pragma unroll\n"
@@ -2597,10 +2601,18 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                      "          // the window is sorted: no lane has a later event to take once none has this one\n"
                      "          if (__ballot(v & !found) == 0ull) break;\n"
                      "#endif\n"
-                     "          bb ^= v ? (1u << ((((uint32_t)kj) >> 12) & 31u)) : 0u;\n"
+                     "          const uint32_t ord = ((uint32_t)kj) >> 12, m = v ? 1u << (ord & 31u) : 0u;\n",
+                     nw, nw);
+                if (nw == 1u)
+                    bput(&b, "          bb[0] ^= m;\n");
+                else
+                    for (uint32_t w = 0; w < nw; ++w) bput(&b, "          bb[%u] ^= (ord >> 5) == %uu ? m : 0u;\n", w, w);
+                bput(&b,
                      "          uint32_t rj;\n"
                      "          {\n"
-                     "            const uint32_t bits[1] = {bb};\n");
+                     "            const uint32_t bits[%u] = {bb[0]", nw);
+                for (uint32_t w = 1; w < nw; ++w) bput(&b, ", bb[%u]", w);
+                bput(&b, "};\n");
                 gen_eval_block(&g, &lut, use_lut, n_recs, 12, "rj");
                 bput(&b,
                      "          }\n"
@@ -2613,12 +2625,12 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
                      "        }\n"
                      "        WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);\n"
                      "        if (found) { wodev::hit_from_key(hk, hr, hit); return true; }\n"
-                     "        bits[0] = bb;\n"
+                     "        for (int w = 0; w < %u; ++w) bits[w] = bb[w];\n"
                      "        if (!win.dropped()) return false;\n"
                      "        after = last;\n"
                      "        WO_WK(WO_WORK_RECOLLECTS);\n"
                      "        win.clear();\n"
-                     "        {\n");
+                     "        {\n", nw);
                 g.first_pass = 0;
                 gen_collect_all(&g, 10);
                 bput(&b,
