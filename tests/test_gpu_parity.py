@@ -613,6 +613,29 @@ def test_big_general_tree_renders_on_the_lanes_while_it_compiles(monkeypatch):
     r.close()
 
 
+def test_kernel_info_names_the_code_object():
+    """wo_renderer_kernel_info: the last launch's code object as the runtime loaded it --
+    the specialised kernel's key (a SHA-256 of source, options and toolchain: another
+    scene, another key), its scratch bytes per lane (csg32's kernel spills nothing) and
+    VGPRs; a lane-tracer launch names its template kind, as lanes_info does.  bench.py
+    records it in every line and keys the committed traffic figures by it."""
+    r, info = _scene("csg32", "auto")
+    assert r.kernel_info() is None  # no path launch yet
+    r.render(info.params(width=64, height=32, spp=1))
+    k = r.kernel_info()
+    assert r.trace_path() == "jit" and len(k["key"]) == 64 and int(k["key"], 16) >= 0
+    assert k["scratch_bytes"] == 0 and 0 < k["vgprs"] <= 64 and k["lds_bytes"] > 0, k
+    r2, info2 = _scene("csg32_nested", "auto")
+    r2.render(info2.params(width=64, height=32, spp=1))
+    assert r2.kernel_info()["key"] != k["key"]
+    r3, info3 = _scene("rtiow_cover", "auto")
+    r3.render(info3.params(width=64, height=32, spp=1))
+    k3 = r3.kernel_info()
+    assert r3.trace_path() == "lanes" and k3["key"] == f"static:{r3.lanes_info()['kind']}", k3
+    for x in (r, r2, r3):
+        x.close()
+
+
 @pytest.mark.parametrize("window", ["lds2", "default"])
 def test_jit_event_windows(window, monkeypatch):
     """The specialised kernel's event windows -- the sorted LDS list (csg32_nested),
