@@ -281,23 +281,30 @@ static void gen_lone_sphere(Gen* g, const WoRec* L, uint32_t ord, int indent) {
          "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(disc) : \"v\"(ll));\n"
          "%*s  if (__ballot(wodev::sphere_need(b, disc)) != 0ull) {\n"
          "%*s    asm volatile(\"\");\n"
+         "#if WO_LONE_SEL_EV  // every lane of the wave forms the interval; hd masks the bit and the events\n"
+         "%*s    {\n"
+         "%*s      const bool hd = !(disc < 0.0f);\n"
+         "#else\n"
          "%*s    if (!(disc < 0.0f)) {\n"
+         "%*s      const bool hd = true;\n"
+         "#endif\n"
          "%*s      const float s = wodev::sqrt_pt(disc), nb = -b, la = nb - s, lb = nb + s;\n"
          "%*s      uint32_t ka, kb;\n"
          "%*s      asm volatile(\"s_mov_b32 %%0, 0x%08x\\n\\ts_mov_b32 %%1, 0x%08x\" : \"=s\"(ka), \"=s\"(kb));\n",
          indent, "", indent, "", indent, "", vl[0], indent, "", vl[1], indent, "", vl[2], indent, "", indent, "", vl[3],
-         indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", ord << 12, (ord << 12) | (1u << 11));
+         indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", indent, "",
+         ord << 12, (ord << 12) | (1u << 11));
     if (g->first_pass)
         bput(g->b,
-             "%*s      bits[%u] |= ((la <= tmin) & (lb > tmin) ? 1u : 0u) << %u;\n"
-             "%*s      { const bool c = la > tmin; WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, wodev::event_key_lo(la, ka)); }\n"
-             "%*s      { const bool c = (lb > tmin) & (lb < wodev::kInf); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, wodev::event_key_lo(lb, kb)); }\n",
+             "%*s      bits[%u] |= (hd & (la <= tmin) & (lb > tmin) ? 1u : 0u) << %u;\n"
+             "%*s      { const bool c = hd & (la > tmin); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, wodev::event_key_lo(la, ka)); }\n"
+             "%*s      { const bool c = hd & (lb > tmin) & (lb < wodev::kInf); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, wodev::event_key_lo(lb, kb)); }\n",
              indent, "", ord / 32, ord % 32, indent, "", indent, "");
     else
         bput(g->b,
              "%*s      const uint64_t k0 = wodev::event_key_lo(la, ka), k1 = wodev::event_key_lo(lb, kb);\n"
-             "%*s      { const bool c = (la > tmin) & (k0 > after); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, k0); }\n"
-             "%*s      { const bool c = (lb > tmin) & (lb < wodev::kInf) & (k1 > after); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, k1); }\n",
+             "%*s      { const bool c = hd & (la > tmin) & (k0 > after); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, k0); }\n"
+             "%*s      { const bool c = hd & (lb > tmin) & (lb < wodev::kInf) & (k1 > after); WO_WK_IF(c, WO_WORK_EVENTS); win.insert_if(c, k1); }\n",
              indent, "", indent, "", indent, "");
     bput(g->b, "%*s    }\n%*s  }\n%*s}\n", indent, "", indent, "", indent, "");
 }
@@ -698,19 +705,25 @@ static void gen_term(Gen* g, const SPrim* q, int indent) {
              "%*s  asm(\"v_sub_f32_e32 %%0, 0x%08x, %%1\" : \"=v\"(disc) : \"v\"(ll));\n"
              "%*s  if (__ballot(wodev::sphere_need(b, disc)) != 0ull) {\n"
              "%*s    asm volatile(\"\");\n"
+             "#if WO_LONE_SEL  // every lane of the wave forms the interval; hd masks the candidates\n"
+             "%*s    {\n"
+             "%*s      const bool hd = !(disc < 0.0f);\n"
+             "#else\n"
              "%*s    if (!(disc < 0.0f)) {\n"
+             "%*s      const bool hd = true;\n"
+             "#endif\n"
              "%*s      const float s = wodev::sqrt_pt(disc), nb = -b, la = nb - s, lb = nb + s;\n"
              "%*s      uint32_t ka, kb;\n"
              "%*s      asm volatile(\"s_mov_b32 %%0, 0x%08x\\n\\ts_mov_b32 %%1, 0x%08x\" : \"=s\"(ka), \"=s\"(kb));\n"
              "%*s      const uint64_t k0 = wodev::event_key_lo(la, ka), k1 = wodev::event_key_lo(lb, kb);\n",
              indent, "", indent, "", indent, "", vl[0], indent, "", vl[1], indent, "", vl[2], indent, "", indent, "",
-             vl[3], indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", term_ka(o0, 1),
-             term_kb(o0, 1), indent, "");
-        if (first) bput(g->b, "%*s      cnt += ((la <= tmin) & (lb > tmin)) ? 1u : 0u;\n", indent, "");
+             vl[3], indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", indent, "", indent, "",
+             indent, "", term_ka(o0, 1), term_kb(o0, 1), indent, "");
+        if (first) bput(g->b, "%*s      cnt += (hd & (la <= tmin) & (lb > tmin)) ? 1u : 0u;\n", indent, "");
         bput(g->b,
              "%*s      WO_WK(WO_WORK_EVENTS);\n"
-             "%*s      wodev::term_cand(k0, (la > tmin)%s, best);\n"
-             "%*s      wodev::term_cand(k1, (lb > tmin) & (lb < wodev::kInf)%s, best);\n"
+             "%*s      wodev::term_cand(k0, hd & (la > tmin)%s, best);\n"
+             "%*s      wodev::term_cand(k1, hd & (lb > tmin) & (lb < wodev::kInf)%s, best);\n"
              "%*s    }\n%*s  }\n%*s}\n",
              indent, "", indent, "", after0, indent, "", after1, indent, "", indent, "", indent, "");
         return;
@@ -2290,6 +2303,9 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * 10.06 -> 10.16; profiles/r06_ab_sweep_unroll.txt) */
     bput(&b, "#ifndef WO_SWEEP_UNROLL\n#define WO_SWEEP_UNROLL 0\n#endif\n");
     bput(&b, "#ifndef WO_SWEEP_BATCH\n#define WO_SWEEP_BATCH 1\n#endif\n#ifndef WO_SWEEP_BATCH_EXIT\n#define WO_SWEEP_BATCH_EXIT 1\n#endif\n");
+    /* term mode's lone spheres: the interval on every lane behind the wave-level test,
+     * masked, instead of a lane branch on disc >= 0 */
+    bput(&b, "#ifndef WO_LONE_SEL\n#define WO_LONE_SEL 1\n#endif\n#ifndef WO_LONE_SEL_EV\n#define WO_LONE_SEL_EV 1\n#endif\n");
     /* the levelled tables' membership words in LDS (wodev::LdsBits) from 4 words; with
      * them csg360_nested's kernel fits 5 waves per SIMD without scratch (the window of
      * 14 keys; 130.2 ms, against 131.6 at 6 waves with 60 B of scratch per lane and
