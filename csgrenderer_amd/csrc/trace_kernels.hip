@@ -43,6 +43,7 @@
 #include "wololo/wo_scene.h"
 
 #include "jit_sources.inc"
+#include "static_key.inc"  // WO_STATIC_SRC_SHA: the library kernels' source identity
 
 #pragma clang fp contract(off)
 
@@ -2864,7 +2865,7 @@ static hipError_t static_attrs(PathKind kind, hipFuncAttributes* a) {
 }
 
 // The path kernel of the last launch: key_hex (65 bytes) gets the specialised
-// kernel's code-object key (jit_key) or "static:<kind>"; out[0] = kind (PathKind),
+// kernel's code-object key (jit_key) or "static:<kind>:<source hash>"; out[0] = kind (PathKind),
 // out[1] = private bytes per lane, out[2] = registers (VGPRs), out[3] = static LDS
 // bytes.  A profile session records these beside its counters, so a summary says
 // which code object it measured.
@@ -2885,12 +2886,13 @@ extern "C" int wo_dev_kernel_info(WoDev* dev, char* key_hex, uint32_t* out) {
         out[3] = (uint32_t)lds;
         if (key_hex) snprintf(key_hex, 65, "%s", dev->jit_key.c_str());
     } else {
+        // "static:<kind>:" + the first 40 hex digits of the library kernels' source hash
         hipFuncAttributes a;
         if (static_attrs<false>(kind, &a) != hipSuccess) return -1;
         out[1] = (uint32_t)a.localSizeBytes;
         out[2] = (uint32_t)a.numRegs;
         out[3] = (uint32_t)a.sharedSizeBytes;
-        if (key_hex) snprintf(key_hex, 65, "static:%u", (unsigned)kind);
+        if (key_hex) snprintf(key_hex, 65, "static:%u:%.40s", (unsigned)kind, WO_STATIC_SRC_SHA);
     }
     return 0;
 }

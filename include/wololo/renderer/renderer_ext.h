@@ -280,7 +280,7 @@ int wo_renderer_jit_info(Wo_Renderer* r, double* seconds);
 int wo_renderer_lanes_info(Wo_Renderer* r, uint32_t* out);
 /* The path kernel of the last launch as the runtime loaded it: key_hex (65 bytes)
  * gets the specialised kernel's code-object key (SHA-256 of source, options and
- * toolchain) or "static:<kind>"; out[0] = kind (as lanes_info's), out[1] = private
+ * toolchain) or "static:<kind>:<40 hex digits of the library kernels' source hash>"; out[0] = kind (as lanes_info's), out[1] = private
  * (scratch) bytes per lane, out[2] = VGPRs, out[3] = static LDS bytes.  Profile
  * sessions record it beside their counters.  0, or -1 before any path launch. */
 int wo_renderer_kernel_info(Wo_Renderer* r, char* key_hex, uint32_t* out);
