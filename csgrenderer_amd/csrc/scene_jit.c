@@ -2305,7 +2305,10 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
     bput(&b, "#ifndef WO_SWEEP_BATCH\n#define WO_SWEEP_BATCH 1\n#endif\n#ifndef WO_SWEEP_BATCH_EXIT\n#define WO_SWEEP_BATCH_EXIT 1\n#endif\n");
     /* term mode's lone spheres: the interval on every lane behind the wave-level test,
      * masked, instead of a lane branch on disc >= 0 */
-    bput(&b, "#ifndef WO_LONE_SEL\n#define WO_LONE_SEL 1\n#endif\n#ifndef WO_LONE_SEL_EV\n#define WO_LONE_SEL_EV 1\n#endif\n");
+    /* (not for the union count: csg256 balanced then spills 48 B per lane at 7 waves, 1.7 GB
+     * of scratch traffic per frame) */
+    bput(&b, "#ifndef WO_LONE_SEL\n#define WO_LONE_SEL 1\n#endif\n#ifndef WO_LONE_SEL_EV\n#define WO_LONE_SEL_EV %d\n#endif\n",
+         n_uterms ? 0 : 1);
     /* the levelled tables' membership words in LDS (wodev::LdsBits) from 4 words; with
      * them csg360_nested's kernel fits 5 waves per SIMD without scratch (the window of
      * 14 keys; 130.2 ms, against 131.6 at 6 waves with 60 B of scratch per lane and
