@@ -1452,6 +1452,7 @@ struct WoDev {
     std::string jit_src;  // its source (the counting variant is built from it on demand)
     hipModule_t count_module;
     hipFunction_t count_fn;
+    int jit_attr[3];  // the loaded specialised kernel's scratch bytes per lane, VGPRs, static LDS (kernel_info)
     int jit_origin;       // 0 process cache, 1 disk cache, 2 compiled
     double jit_compile_sec;
 };
@@ -2630,6 +2631,12 @@ extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t err
     dev->jit_module = mod;
     dev->jit_fn = fn;
     dev->jit_key = key;
+    // its resources, read now: once the counting variant (the same kernel name in another
+    // module) is loaded, an attribute query of this function returned that one's scratch size
+    dev->jit_attr[0] = dev->jit_attr[1] = dev->jit_attr[2] = -1;
+    (void)hipFuncGetAttribute(&dev->jit_attr[0], HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, fn);
+    (void)hipFuncGetAttribute(&dev->jit_attr[1], HIP_FUNC_ATTRIBUTE_NUM_REGS, fn);
+    (void)hipFuncGetAttribute(&dev->jit_attr[2], HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, fn);
     dev->jit_src = src;
     {
         const char* m = strstr(src, "// wo_share_tiles ");
@@ -2875,15 +2882,10 @@ extern "C" int wo_dev_kernel_info(WoDev* dev, char* key_hex, uint32_t* out) {
     if (hipSetDevice(dev->device) != hipSuccess) return -1;
     out[0] = (uint32_t)kind;
     if (kind == kJit) {
-        if (!dev->jit_fn) return -1;
-        int local = 0, regs = 0, lds = 0;
-        if (hipFuncGetAttribute(&local, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, dev->jit_fn) != hipSuccess ||
-            hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, dev->jit_fn) != hipSuccess ||
-            hipFuncGetAttribute(&lds, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, dev->jit_fn) != hipSuccess)
-            return -1;
-        out[1] = (uint32_t)local;
-        out[2] = (uint32_t)regs;
-        out[3] = (uint32_t)lds;
+        if (!dev->jit_fn || dev->jit_attr[0] < 0 || dev->jit_attr[1] < 0 || dev->jit_attr[2] < 0) return -1;
+        out[1] = (uint32_t)dev->jit_attr[0];  // read when the module was loaded (wo_dev_set_jit)
+        out[2] = (uint32_t)dev->jit_attr[1];
+        out[3] = (uint32_t)dev->jit_attr[2];
         if (key_hex) snprintf(key_hex, 65, "%s", dev->jit_key.c_str());
     } else {
         // "static:<kind>:" + the first 40 hex digits of the library kernels' source hash

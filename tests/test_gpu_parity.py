@@ -625,6 +625,9 @@ def test_kernel_info_names_the_code_object():
     k = r.kernel_info()
     assert r.trace_path() == "jit" and len(k["key"]) == 64 and int(k["key"], 16) >= 0
     assert k["scratch_bytes"] == 0 and 0 < k["vgprs"] <= 64 and k["lds_bytes"] > 0, k
+    # the counting variant (same kernel name, another module) does not change what it reports
+    r.count_work(info.params(width=64, height=32, spp=1))
+    assert r.kernel_info() == k, (r.kernel_info(), k)
     r2, info2 = _scene("csg32_nested", "auto")
     r2.render(info2.params(width=64, height=32, spp=1))
     assert r2.kernel_info()["key"] != k["key"]
