@@ -129,17 +129,8 @@ static void gen_members(Gen* g, uint32_t pc, uint32_t cnt, int indent) {
         const WoRec* L = &g->prog[pc + 1 + m];
         uint32_t vl[4];
         for (int i = 0; i < 4; ++i) vl[i] = fbits(L->f[i]);
-        /* empty, or ending at or before t_min, on every lane: the other members cannot
-         * widen it (a met interval only narrows), and every consumer of the interval
-         * reads it only through b > t_min (no event, not inside at t_min, not a valid
-         * term literal) -- so stopping here gives the same bits, events and candidates
-         * (round 6: the exit-before-t_min half, WO_MEMBER_SKIP_BEHIND) */
-        if (m > 0)
-            bput(g->b,
-                 "#if WO_MEMBER_SKIP_BEHIND\n%*s  if (__ballot(!(iv.a > iv.b) & (iv.b > tmin)) != 0ull) {\n#else\n"
-                 "%*s  if (__ballot(!(iv.a > iv.b)) != 0ull) {\n#endif\n",
-                 indent, "", indent, ""),
-                ++open_skips;
+        if (m > 0) /* empty on every lane: the other members cannot widen it */
+            bput(g->b, "%*s  if (__ballot(!(iv.a > iv.b)) != 0ull) {\n", indent, ""), ++open_skips;
         bput(g->b, "%*s  {\n", indent, "");
         const WoRec* L2 = m + 1u < cnt ? &g->prog[pc + 2 + m] : NULL;
         if (L->op == WO_LEAF_HALFSPACE && L->u1 != 0u && L2 && L2->op == WO_LEAF_HALFSPACE &&
@@ -2318,9 +2309,6 @@ char* wo_generate_jit_source(WoRec const* prog, uint32_t n_recs, uint32_t n_prim
      * of scratch traffic per frame) */
     bput(&b, "#ifndef WO_LONE_SEL\n#define WO_LONE_SEL 1\n#endif\n#ifndef WO_LONE_SEL_EV\n#define WO_LONE_SEL_EV %d\n#endif\n",
          n_uterms ? 0 : 1);
-    /* (measured: csg32 2.590 / 2.601 ms with / without, nested 6.26 / 6.24, balanced 8.31 / 8.27:
-     * no gain, off; profiles/r06_ab_member_skip_behind.txt) */
-    bput(&b, "#ifndef WO_MEMBER_SKIP_BEHIND\n#define WO_MEMBER_SKIP_BEHIND 0\n#endif\n");
     /* the levelled tables' membership words in LDS (wodev::LdsBits) from 4 words; with
      * them csg360_nested's kernel fits 5 waves per SIMD without scratch (the window of
      * 14 keys; 130.2 ms, against 131.6 at 6 waves with 60 B of scratch per lane and
