@@ -388,6 +388,14 @@ __device__ __forceinline__ float box_near(float4 lo, float4 hi, F3 ri, F3 oi, fl
 #define WO_LANES_GWIN 32
 #endif
 constexpr int kGWin = WO_LANES_GWIN;
+// a walk trip's node steps, then the leaf they reached, in one trip (LaneTracer::trip;
+// the same steps per lane in the same order); 0 leaf phases: a trip is a node or a leaf
+#ifndef WO_LANES_TRIP_NODES
+#define WO_LANES_TRIP_NODES 2
+#endif
+#ifndef WO_LANES_TRIP_LEAVES
+#define WO_LANES_TRIP_LEAVES 1
+#endif
 // a general tree's node record (build_lbvh): left ref | right ref << 15 | op << 30
 constexpr uint32_t kGRefBits = 15u, kGRefMask = (1u << kGRefBits) - 1u;
 template <int kModeT, bool kCountT>
@@ -722,121 +730,144 @@ struct LaneTracer {
 
     // One trip of the walk: a leaf, or a node (its children's boxes, nearest hit
     // child next, the other(s) pushed); then a pop when the walk has no next node.
+    // WO_LANES_TRIP_NODES node steps and then WO_LANES_TRIP_LEAVES leaves in one trip:
+    // a lane walks node -> node -> leaf in one trip instead of three, so the wave's
+    // lanes, at different depths, still share most trips' node and leaf code.
     __device__ __forceinline__ void trip(QState& s, F3 o, F3 d, F3 ri, F3 oi, F3& inv, bool& have_inv) {
         WO_WK_WAVE(WO_WORK_SWEEP_TRIPS);  // lane tracer: walk trips per wave
         uint32_t cur = s.cur, sp = s.sp;
         const float tlo = s.tlo;
-        if (cur & kLeafRef) {
-            visit_leaf(cur & ~kLeafRef, s.cnt, s, o, d, inv, have_inv);
-            cur = kNoRef;
-        } else if constexpr (kWide) {
-            // four children: lo.x, hi.x, lo.y, hi.y, lo.z, hi.z of each, then the refs
-            WO_WK_N(WO_WORK_BOUND_TESTS, 4u);
-            float4 q[7];
-#if WO_LANES_PRIO
-            __builtin_amdgcn_s_setprio(WO_LANES_PRIO);
-#endif
-            if (cur < ntop) {
-                const LdsNodes nd = ltop + 7u * cur;
-#pragma unroll
-                for (int k = 0; k < 7; ++k) q[k] = nd[k];
-                asm volatile("");
-            } else {
-                const GlobalNodes nd = (GlobalNodes)lnodes + 7u * cur;
-#pragma unroll
-                for (int k = 0; k < 7; ++k) q[k] = nd[k];
-            }
-#if WO_LANES_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
-            const float tb = s.best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(s.best >> 32));
-            // per child a sort key: the top 16 bits of max(near, 0) (monotone as an
-            // unsigned integer; the order only steers the walk) | the child's 16-bit
-            // ref; ~0 for a miss or an empty slot
-            uint32_t kk[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float ax = __builtin_fmaf(f4c(q[0], c), ri.x, -oi.x), bx = __builtin_fmaf(f4c(q[1], c), ri.x, -oi.x);
-                const float ay = __builtin_fmaf(f4c(q[2], c), ri.y, -oi.y), by = __builtin_fmaf(f4c(q[3], c), ri.y, -oi.y);
-                const float az = __builtin_fmaf(f4c(q[4], c), ri.z, -oi.z), bz = __builtin_fmaf(f4c(q[5], c), ri.z, -oi.z);
-                const float n = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-                const float f = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-                const uint32_t r16 = __float_as_uint(f4c(q[6], c));
-                const float n0 = fmaxf(n, 0.0f);
-                const bool h = (f >= fmaxf(n0, tlo)) & (n <= tb) & (r16 != kNoRef16);
-                kk[c] = h ? ((__float_as_uint(n0) & 0xffff0000u) | r16) : 0xffffffffu;
-            }
-            // nearest first: a 4-key sorting network (misses sort last)
-            auto ce = [&](int i, int j) {
-                const uint32_t lo = kk[i] < kk[j] ? kk[i] : kk[j], hi = kk[i] < kk[j] ? kk[j] : kk[i];
-                kk[i] = lo;
-                kk[j] = hi;
-            };
-            ce(0, 1);
-            ce(2, 3);
-            ce(0, 2);
-            ce(1, 3);
-            ce(1, 2);
-            cur = kk[0] == 0xffffffffu ? kNoRef : (kk[0] & 0x7fffu) | ((kk[0] & 0x8000u) << 16);
-            // the farther ones on the stack, farthest deepest (sp < 3 x the tree's levels)
-#pragma unroll
-            for (int c = 3; c >= 1; --c) {
-                if (kk[c] != 0xffffffffu) {
-                    stk16[sp * kBlock] = (uint16_t)kk[c];
-                    ++sp;
+        auto pop = [&]() {
+            if ((cur == kNoRef) & (sp != 0u)) {
+                --sp;
+                if constexpr (kStack16) {
+                    const uint32_t e = stk16[sp * kBlock];
+                    cur = (e & 0x7fffu) | ((e & 0x8000u) << 16);
+                } else {
+                    cur = stk[sp * kBlock];
                 }
             }
-        } else {
-            WO_WK_N(WO_WORK_BOUND_TESTS, 2u);
-            float na, nb, fa, fb;
-            uint32_t ra, rb;
-            {
-                float4 a0, a1, b0, b1;
+        };
+        // a leaf (not the walk's end) visited, then the next entry popped
+        auto leaf_phase = [&]() {
+            if (((cur & kLeafRef) != 0u) & (cur != kNoRef)) {
+                visit_leaf(cur & ~kLeafRef, s.cnt, s, o, d, inv, have_inv);
+                cur = kNoRef;
+                pop();
+            }
+        };
+        // the node step (the non-fused walk: or the leaf), then a pop when it ends a path
+        auto node_phase = [&]() {
+            const bool at_leaf = (cur & kLeafRef) != 0u;  // (the walk's end, kNoRef, included)
+            if (!WO_LANES_TRIP_LEAVES && at_leaf) {
+                visit_leaf(cur & ~kLeafRef, s.cnt, s, o, d, inv, have_inv);
+                cur = kNoRef;
+            } else if (kWide && !at_leaf) {
+                // four children: lo.x, hi.x, lo.y, hi.y, lo.z, hi.z of each, then the refs
+                WO_WK_N(WO_WORK_BOUND_TESTS, 4u);
+                float4 q[7];
 #if WO_LANES_PRIO
-                __builtin_amdgcn_s_setprio(WO_LANES_PRIO);  // a wave about to issue its node load goes first
+                __builtin_amdgcn_s_setprio(WO_LANES_PRIO);
 #endif
-                if (cur < ntop) {  // the top levels: LDS latency instead of a cache round trip
-                    const LdsNodes nd = ltop + 4u * cur;
-                    a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
-                    asm volatile("");  // the branches' tails differ: the loads are not merged into flat loads
+                if (cur < ntop) {
+                    const LdsNodes nd = ltop + 7u * cur;
+#pragma unroll
+                    for (int k = 0; k < 7; ++k) q[k] = nd[k];
+                    asm volatile("");
                 } else {
-                    const GlobalNodes nd = (GlobalNodes)lnodes + 4u * cur;
-                    a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                    const GlobalNodes nd = (GlobalNodes)lnodes + 7u * cur;
+#pragma unroll
+                    for (int k = 0; k < 7; ++k) q[k] = nd[k];
                 }
 #if WO_LANES_PRIO
                 __builtin_amdgcn_s_setprio(0);
 #endif
-                na = box_near(a0, a1, ri, oi, fa);
-                nb = box_near(b0, b1, ri, oi, fb);
-                ra = __float_as_uint(a0.w);
-                rb = __float_as_uint(a1.w);
+                const float tb = s.best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(s.best >> 32));
+                // per child a sort key: the top 16 bits of max(near, 0) (monotone as an
+                // unsigned integer; the order only steers the walk) | the child's 16-bit
+                // ref; ~0 for a miss or an empty slot
+                uint32_t kk[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float ax = __builtin_fmaf(f4c(q[0], c), ri.x, -oi.x), bx = __builtin_fmaf(f4c(q[1], c), ri.x, -oi.x);
+                    const float ay = __builtin_fmaf(f4c(q[2], c), ri.y, -oi.y), by = __builtin_fmaf(f4c(q[3], c), ri.y, -oi.y);
+                    const float az = __builtin_fmaf(f4c(q[4], c), ri.z, -oi.z), bz = __builtin_fmaf(f4c(q[5], c), ri.z, -oi.z);
+                    const float n = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                    const float f = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                    const uint32_t r16 = __float_as_uint(f4c(q[6], c));
+                    const float n0 = fmaxf(n, 0.0f);
+                    const bool h = (f >= fmaxf(n0, tlo)) & (n <= tb) & (r16 != kNoRef16);
+                    kk[c] = h ? ((__float_as_uint(n0) & 0xffff0000u) | r16) : 0xffffffffu;
+                }
+                // nearest first: a 4-key sorting network (misses sort last)
+                auto ce = [&](int i, int j) {
+                    const uint32_t lo = kk[i] < kk[j] ? kk[i] : kk[j], hi = kk[i] < kk[j] ? kk[j] : kk[i];
+                    kk[i] = lo;
+                    kk[j] = hi;
+                };
+                ce(0, 1);
+                ce(2, 3);
+                ce(0, 2);
+                ce(1, 3);
+                ce(1, 2);
+                cur = kk[0] == 0xffffffffu ? kNoRef : (kk[0] & 0x7fffu) | ((kk[0] & 0x8000u) << 16);
+                // the farther ones on the stack, farthest deepest (sp < 3 x the tree's levels)
+#pragma unroll
+                for (int c = 3; c >= 1; --c) {
+                    if (kk[c] != 0xffffffffu) {
+                        stk16[sp * kBlock] = (uint16_t)kk[c];
+                        ++sp;
+                    }
+                }
+            } else if (!kWide && !at_leaf) {
+                WO_WK_N(WO_WORK_BOUND_TESTS, 2u);
+                float na, nb, fa, fb;
+                uint32_t ra, rb;
+                {
+                    float4 a0, a1, b0, b1;
+#if WO_LANES_PRIO
+                    __builtin_amdgcn_s_setprio(WO_LANES_PRIO);  // a wave about to issue its node load goes first
+#endif
+                    if (cur < ntop) {  // the top levels: LDS latency instead of a cache round trip
+                        const LdsNodes nd = ltop + 4u * cur;
+                        a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                        asm volatile("");  // the branches' tails differ: the loads are not merged into flat loads
+                    } else {
+                        const GlobalNodes nd = (GlobalNodes)lnodes + 4u * cur;
+                        a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3];
+                    }
+#if WO_LANES_PRIO
+                    __builtin_amdgcn_s_setprio(0);
+#endif
+                    na = box_near(a0, a1, ri, oi, fa);
+                    nb = box_near(b0, b1, ri, oi, fb);
+                    ra = __float_as_uint(a0.w);
+                    rb = __float_as_uint(a1.w);
+                }
+                // useful range: up to the best event so far
+                const float tb = s.best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(s.best >> 32));
+                const bool ha = (fa >= fmaxf(na, tlo)) & (na <= tb);
+                const bool hb = (fb >= fmaxf(nb, tlo)) & (nb <= tb);
+                if (ha & hb) {
+                    const bool a_first = na <= nb;
+                    cur = a_first ? ra : rb;
+                    const uint32_t other = a_first ? rb : ra;
+                    if constexpr (kStack16)  // refs < 2^15 (build_lbvh): the leaf flag moves to bit 15
+                        stk16[sp * kBlock] = (uint16_t)((other & 0x7fffu) | ((other >> 16) & 0x8000u));
+                    else
+                        stk[sp * kBlock] = other;  // sp < the tree's depth (build_lbvh)
+                    ++sp;
+                } else {
+                    cur = ha ? ra : (hb ? rb : kNoRef);
+                }
             }
-            // useful range: up to the best event so far
-            const float tb = s.best == kEmptyKey ? kInf : __uint_as_float((uint32_t)(s.best >> 32));
-            const bool ha = (fa >= fmaxf(na, tlo)) & (na <= tb);
-            const bool hb = (fb >= fmaxf(nb, tlo)) & (nb <= tb);
-            if (ha & hb) {
-                const bool a_first = na <= nb;
-                cur = a_first ? ra : rb;
-                const uint32_t other = a_first ? rb : ra;
-                if constexpr (kStack16)  // refs < 2^15 (build_lbvh): the leaf flag moves to bit 15
-                    stk16[sp * kBlock] = (uint16_t)((other & 0x7fffu) | ((other >> 16) & 0x8000u));
-                else
-                    stk[sp * kBlock] = other;  // sp < the tree's depth (build_lbvh)
-                ++sp;
-            } else {
-                cur = ha ? ra : (hb ? rb : kNoRef);
-            }
-        }
-        if ((cur == kNoRef) & (sp != 0u)) {
-            --sp;
-            if constexpr (kStack16) {
-                const uint32_t e = stk16[sp * kBlock];
-                cur = (e & 0x7fffu) | ((e & 0x8000u) << 16);
-            } else {
-                cur = stk[sp * kBlock];
-            }
-        }
+            pop();
+        };
+        // (a lane at a leaf or at the walk's end skips a node step)
+#pragma unroll
+        for (int k = 0; k < WO_LANES_TRIP_NODES; ++k) node_phase();
+#pragma unroll
+        for (int k = 0; k < WO_LANES_TRIP_LEAVES; ++k) leaf_phase();
         s.cur = cur;
         s.sp = sp;
     }
@@ -2351,7 +2382,13 @@ static LaneBvh lane_bvh(const WoDev* dev) {
     b.nprims = dev->lb_nprims;
     b.ntop = dev->lb_top;
     b.depth = dev->lb_depth;
-    b.dyn_walkers = 24u;  // csg512_balanced: 60.4 / 57.6 / 57.2 / 58.1 / 59.2 ms at 8 / 16 / 24 / 32 / 40
+    // csg512_balanced: 60.4 / 57.6 / 57.2 / 58.1 / 59.2 ms at 8 / 16 / 24 / 32 / 40;
+    // WOLOLO_DYN_WALKERS (measurement) overrides
+    static const uint32_t walkers = [] {
+        const char* w = getenv("WOLOLO_DYN_WALKERS");
+        return w && *w ? (uint32_t)atoi(w) : 24u;
+    }();
+    b.dyn_walkers = walkers;
     b.trec = dev->lb_terms ? reinterpret_cast<const float4*>(reinterpret_cast<const uint32_t*>(dev->d_lbvh) +
                                                             dev->lb_term_off)
                            : nullptr;
