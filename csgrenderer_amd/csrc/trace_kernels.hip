@@ -1471,6 +1471,12 @@ struct WoDev {
     float4* h_part[WO_SLOTS];  // WO_PEER_STAGED: the share's pinned host copy
     size_t hpart_cap[WO_SLOTS];
     hipEvent_t part_ev[WO_SLOTS];
+    // the split present (present_rows): this rank's rows encoded for present, and the
+    // events that order its encode after its render (psrc), the gather's reuse of
+    // the share after the encode (penc) and the root's slot after the D2H (pmap)
+    uint32_t* d_pbgra[WO_SLOTS];
+    size_t dpbgra_cap[WO_SLOTS];
+    hipEvent_t psrc_ev[WO_SLOTS], penc_ev[WO_SLOTS], pmap_ev[WO_SLOTS];
     int peer_mode;  // how this rank's share reaches the root (WO_PEER_*; wo_dev_enable_peer)
     unsigned long long* d_segacc;  // segments of this rank's device frames (wo_dev_take_segments)
     bool union_only;
@@ -1583,6 +1589,9 @@ extern "C" void wo_dev_destroy(WoDev* dev) {
         if (dev->gate_ev[i]) (void)hipEventDestroy(dev->gate_ev[i]);
         if (dev->d_part[i]) (void)hipFree(dev->d_part[i]);
         if (dev->part_ev[i]) (void)hipEventDestroy(dev->part_ev[i]);
+        if (dev->d_pbgra[i]) (void)hipFree(dev->d_pbgra[i]);
+        for (hipEvent_t ev : {dev->psrc_ev[i], dev->penc_ev[i], dev->pmap_ev[i]})
+            if (ev) (void)hipEventDestroy(ev);
         if (dev->rend_ev[i]) (void)hipEventDestroy(dev->rend_ev[i]);
         for (int k = 0; k < 3; ++k)
             if (dev->st_ev[i][k]) (void)hipEventDestroy(dev->st_ev[i][k]);
@@ -3295,7 +3304,10 @@ static int open_slot(WoDev* dev, int slot, char* err, size_t errlen) {
 // stream -- the present encode, its copy to pinned host memory and, when
 // `map_float`, the float frame's copy -- then the slot event.  The render stream
 // does not wait for any of it: the next frame's kernel starts at once.
-static int present_slot(WoDev* dev, int slot, size_t pixels, bool map_float, char* err, size_t errlen) {
+// `encoded`: the ranks have already written the present encode into h_bgra (the
+// split present, wo_dev_frame_submit_ranks); only the float frame is left.
+static int present_slot(WoDev* dev, int slot, size_t pixels, bool map_float, char* err, size_t errlen,
+                        bool encoded = false) {
     hipError_t e = dev->stamps ? hipEventRecord(dev->st_ev[slot][1], dev->stream) : hipSuccess;
     if (e == hipSuccess) e = hipEventRecord(dev->rend_ev[slot], dev->stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(dev->copy_stream, dev->rend_ev[slot], 0);
@@ -3308,9 +3320,11 @@ static int present_slot(WoDev* dev, int slot, size_t pixels, bool map_float, cha
     if (pixels) {
         // the present encode (wo_renderer_last_frame_bgra8) and, eagerly or on
         // demand (wo_dev_frame_map_float), the float frame (wo_renderer_last_frame)
-        if (wo_dev_srgb8(dev->d_slot[slot], dev->d_bgra[slot], pixels, dev->copy_stream, err, errlen)) return -1;
-        e = hipMemcpyAsync(dev->h_bgra[slot], dev->d_bgra[slot], pixels * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                           dev->copy_stream);
+        if (!encoded) {
+            if (wo_dev_srgb8(dev->d_slot[slot], dev->d_bgra[slot], pixels, dev->copy_stream, err, errlen)) return -1;
+            e = hipMemcpyAsync(dev->h_bgra[slot], dev->d_bgra[slot], pixels * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               dev->copy_stream);
+        }
         if (e == hipSuccess && map_float)
             e = hipMemcpyAsync(dev->h_slot[slot], dev->d_slot[slot], pixels * sizeof(float4), hipMemcpyDeviceToHost,
                                dev->copy_stream);
@@ -3469,9 +3483,68 @@ extern "C" int wo_dev_enable_peer(WoDev* from, WoDev* to, char* err, size_t errl
 // for every part, then un-interleaves the gathered shares into dst.  The root's
 // own share renders on root->stream, straight into its slice of the gather buffer
 // (an event orders it when s_out is another stream).  Asynchronous throughout.
+// The split present (wo_dev_frame_submit_ranks, WOLOLO_PRESENT_SPLIT=1): rank `rank`
+// encodes its own rows for present (srgb8_kernel, the same code per pixel as the
+// whole frame's encode) on its copy stream, after its render, and copies them
+// straight into the root's pinned frame `h_frame`: its full 4-row bands in one 2D
+// copy (band lb is frame band lb * n + rank), a partial last band on its own.  So
+// each rank's D2H is 1/n of the frame, over its own link, instead of the root
+// copying the whole encoded frame.  Current device: the rank's.
+static int present_rows(WoDev* dv, int slot, uint32_t rank, uint32_t n, const WoFrame& fr, const float4* d_rows,
+                        hipStream_t src_stream, uint32_t* h_frame, char* err, size_t errlen) {
+    const uint32_t T = fr.tile_rows, W = fr.width, H = fr.height;
+    const uint32_t lr = wo_rank_local_rows(H, T, n);
+    if (ensure_buffer(&dv->d_pbgra[slot], &dv->dpbgra_cap[slot], (size_t)lr * W * sizeof(uint32_t), err, errlen))
+        return -1;
+    if (ensure_event(&dv->psrc_ev[slot], err, errlen) || ensure_event(&dv->penc_ev[slot], err, errlen) ||
+        ensure_event(&dv->pmap_ev[slot], err, errlen))
+        return -1;
+    const uint32_t cnt = wo_rank_tile_count(H, T, rank, n);
+    hipError_t e = hipEventRecord(dv->psrc_ev[slot], src_stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(dv->copy_stream, dv->psrc_ev[slot], 0);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "split present gate", e);
+        return -1;
+    }
+    if (cnt && wo_dev_srgb8(d_rows, dv->d_pbgra[slot], (size_t)cnt * T * W, dv->copy_stream, err, errlen)) return -1;
+    e = hipEventRecord(dv->penc_ev[slot], dv->copy_stream);
+    if (e == hipSuccess && cnt) {
+        const uint32_t g_last = (cnt - 1u) * n + rank;
+        const bool partial = (g_last + 1u) * T > H;
+        const uint32_t full = cnt - (partial ? 1u : 0u);
+        const size_t band = (size_t)T * W * sizeof(uint32_t);
+        if (full)
+            e = hipMemcpy2DAsync(h_frame + (size_t)rank * T * W, band * n, dv->d_pbgra[slot], band, band, full,
+                                 hipMemcpyDeviceToHost, dv->copy_stream);
+        if (e == hipSuccess && partial)
+            e = hipMemcpyAsync(h_frame + (size_t)g_last * T * W, dv->d_pbgra[slot] + (size_t)(cnt - 1u) * T * W,
+                               (size_t)(H - g_last * T) * W * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               dv->copy_stream);
+    }
+    if (e == hipSuccess) e = hipEventRecord(dv->pmap_ev[slot], dv->copy_stream);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "split present copy", e);
+        return -1;
+    }
+    return 0;
+}
+
+// Off by default: in tools/root_step.py's N = 8 model (csg32, band 2:1) the other
+// ranks' shares took 0.447 ms with their encode + D2H against 0.384 without, and
+// rank 0's step stayed between 0.30 and 0.55 ms either way (profiles/r06_split_present.log)
+static bool present_split_on() {
+    static const bool on = [] {
+        const char* v = getenv("WOLOLO_PRESENT_SPLIT");
+        return v && *v == '1';
+    }();
+    return on;
+}
+
+// `h_present` (the split present): every rank also encodes its rows into the root's
+// pinned frame (present_rows); nullptr: the frame is only assembled.
 static int ranks_render_assemble(WoDev* const* devs, uint32_t n, WoFrame fr, int slot, long long* const* d_accum,
                                  uint32_t accum_spp, hipStream_t s_out, float4* dst, bool count_segments, char* err,
-                                 size_t errlen) {
+                                 size_t errlen, uint32_t* h_present = nullptr) {
     WoDev* root = devs[0];
     fr.tile_rows = 4;
     fr.nranks = n;
@@ -3521,6 +3594,8 @@ static int ranks_render_assemble(WoDev* const* devs, uint32_t n, WoFrame fr, int
     if (wo_dev_launch_ex(root, &fr, root->d_gather[slot], root->stream, seg0, d_accum ? d_accum[0] : nullptr,
                          accum_spp, err, errlen))
         return -1;
+    if (h_present && present_rows(root, slot, 0u, n, fr, root->d_gather[slot], root->stream, h_present, err, errlen))
+        return -1;
     if (own_stream) {
         e = hipEventRecord(root->part_ev[slot], root->stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(s_out, root->part_ev[slot], 0);
@@ -3553,6 +3628,8 @@ static int ranks_render_assemble(WoDev* const* devs, uint32_t n, WoFrame fr, int
         if (wo_dev_launch_ex(dv, &fr, dv->d_part[slot], dv->stream, seg, d_accum ? d_accum[i] : nullptr, accum_spp,
                              err, errlen))
             return -1;
+        if (h_present && present_rows(dv, slot, i, n, fr, dv->d_part[slot], dv->stream, h_present, err, errlen))
+            return -1;
         float4* slice = root->d_gather[slot] + share * i;
         if (staged)  // device -> pinned host on the rank, host -> root below
             e = hipMemcpyAsync(dv->h_part[slot], dv->d_part[slot], share * sizeof(float4), hipMemcpyDeviceToHost,
@@ -3574,8 +3651,10 @@ static int ranks_render_assemble(WoDev* const* devs, uint32_t n, WoFrame fr, int
     }
     if (wo_dev_assemble(root->d_gather[slot], dst, fr.width, fr.height, fr.tile_rows, n, 0u, 0u, s_out, err, errlen))
         return -1;
-    // the slot's buffers are free once the assembly has read them
-    e = hipEventRecord(root->gate_ev[slot], s_out);
+    // the slot's buffers are free once the assembly (and the split present's
+    // encodes) have read them
+    for (uint32_t i = 0; h_present && i < n && e == hipSuccess; ++i) e = hipStreamWaitEvent(s_out, devs[i]->penc_ev[slot], 0);
+    if (e == hipSuccess) e = hipEventRecord(root->gate_ev[slot], s_out);
     if (e != hipSuccess) {
         set_err(err, errlen, "hipEventRecord(gate)", e);
         return -1;
@@ -3603,10 +3682,22 @@ extern "C" int wo_dev_frame_submit_ranks(WoDev* const* devs, uint32_t n, WoFrame
     }
     if (prep_slot(root, slot, frame->width, frame->height, frame->height, err, errlen)) return -1;
     if (open_slot(root, slot, err, errlen)) return -1;
+    const size_t pixels = (size_t)frame->width * frame->height;
+    const bool split = present_split_on() && pixels;
     if (ranks_render_assemble(devs, n, *frame, slot, d_accum, accum_spp, root->stream, root->d_slot[slot], false, err,
-                              errlen))
+                              errlen, split ? root->h_bgra[slot] : nullptr))
         return -1;
-    return present_slot(root, slot, (size_t)frame->width * frame->height, map_float != 0, err, errlen);
+    if (!split) return present_slot(root, slot, pixels, map_float != 0, err, errlen);
+    // the split present: the encoded frame is already on its way to h_bgra from
+    // every rank; the slot's map-back ends when all of those copies have (and the
+    // float frame's, when it is mapped eagerly, after the assembly)
+    e = hipSetDevice(root->device);
+    for (uint32_t i = 0; i < n && e == hipSuccess; ++i) e = hipStreamWaitEvent(root->copy_stream, devs[i]->pmap_ev[slot], 0);
+    if (e != hipSuccess) {
+        set_err(err, errlen, "split present wait", e);
+        return -1;
+    }
+    return present_slot(root, slot, pixels, map_float != 0, err, errlen, /*encoded=*/true);
 }
 
 extern "C" int wo_dev_frame_ranks_device(WoDev* const* devs, uint32_t n, WoFrame const* frame, int slot, void* d_frame,

@@ -164,6 +164,46 @@ def test_multi_rank_renderer_equals_one_device(nranks):
     r.close()
 
 
+_SPLIT_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from csgrenderer_amd import scenes
+from csgrenderer_amd import wololo as wl
+r = wl.Renderer("split", max_nodes=4096)
+info = scenes.build("csg32", r)
+for n, (w, h) in ((3, (203, 117)), (8, (96, 45)), (2, (64, 36))):
+    p = info.params(width=w, height=h, spp=2, seed=7)
+    one = r.render(p)
+    assert r.set_devices(n) == n
+    r.set_draw_params(p)
+    for _ in range(3):
+        r.draw_frame()
+    r.finish()
+    assert np.array_equal(r.last_frame_bgra8(), wl.srgb8_encode_host(one)), (n, w, h)
+    assert np.array_equal(r.last_frame(), one), (n, w, h)
+    assert r.set_devices(1) == 1
+    assert wl.last_error() == "", wl.last_error()
+r.close()
+print("split present ok")
+"""
+
+
+def test_split_present_equals_one_device():
+    """WOLOLO_PRESENT_SPLIT=1: every rank encodes its own rows and copies them into the
+    root's pinned frame (a 2D copy of its full 4-row bands, the partial last band on
+    its own) -- the presented frame equals one device's encode bit for bit, for
+    heights with a partial last band at 3 and 8 ranks.  A subprocess, since the knob
+    is read once per process."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WOLOLO_PRESENT_SPLIT="1")
+    out = subprocess.run([sys.executable, "-c", _SPLIT_SCRIPT, root], env=env, capture_output=True, text=True,
+                         timeout=110)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    assert "split present ok" in out.stdout
+
+
 def test_multi_rank_lanes_and_scene_change():
     """Union-only scene on the lane tracer over 4 ranks; then a node is added with a
     frame in flight: every rank gets the new scene before the next frame."""

@@ -59,8 +59,11 @@ def main():
                          "(bench.py before round 5: its kernels leave the two render streams on one hardware "
                          "queue, so consecutive frames stop overlapping); 'split' = separate copy / assemble / "
                          "D2H streams (rounds 3-5)")
-    ap.add_argument("--map-back", default="bgra", choices=["bgra", "float", "none"],
-                    help="rank 0's D2H of the presented frame after the encode (draw_frame: bgra)")
+    ap.add_argument("--map-back", default="bgra", choices=["split", "bgra", "float", "none"],
+                    help="the presented frame's D2H: 'bgra' = rank 0 encodes and copies the whole frame after "
+                         "the assembly (draw_frame's default); 'split' = every rank encodes its own rows and "
+                         "copies them to the host (WOLOLO_PRESENT_SPLIT=1); 'float' adds the float frame; "
+                         "'none' skips it")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process, as bench.py sets it at N > 1 (0: leave it)")
     args = ap.parse_args()
@@ -103,9 +106,28 @@ def main():
 
     t1 = timed(one_gpu)
     print(f"[root] N=1 {t1:.3f} ms per frame", flush=True)
+    # this box's pinned D2H rate at the whole present frame and at one rank's share of it
+    d2h = {}
+    for mb_bytes in (W * H * 4, W * H * 4 // 8):
+        dsrc = torch.empty(mb_bytes // 4, dtype=torch.int32, device="cuda")
+        hdst = torch.empty(mb_bytes // 4, dtype=torch.int32).pin_memory()
+        hdst.copy_(dsrc, non_blocking=True)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(main_s)
+        for _ in range(20):
+            hdst.copy_(dsrc, non_blocking=True)
+        b.record(main_s)
+        b.synchronize()
+        ms = a.elapsed_time(b) / 20
+        d2h[mb_bytes] = (ms, mb_bytes / ms / 1e6)
+    print("[root] pinned D2H: " + ", ".join(f"{k / 1e6:.2f} MB {v[0] * 1e3:.0f} us ({v[1]:.1f} GB/s)"
+                                           for k, v in d2h.items()), flush=True)
     res = {"scene": args.scene, "size": f"{W}x{H}x{p.spp}", "path": r.trace_path(), "one_gpu_ms": round(t1, 4),
+           "d2h_gbps": {str(k): round(v[1], 2) for k, v in d2h.items()},
            "encode": not args.no_encode, "map_back": "none" if args.no_encode else args.map_back, "worlds": {}}
-    mapback = not args.no_encode and args.map_back != "none"
+    split = not args.no_encode and args.map_back == "split"
+    mapback = not args.no_encode and args.map_back not in ("none", "split")
     hb = [torch.empty((H, W), dtype=torch.int32).pin_memory() for _ in range(2)] if mapback else []
     hf = [torch.empty((H, W, 4), dtype=torch.float32).pin_memory() for _ in range(2)] \
         if mapback and args.map_back == "float" else []
@@ -125,20 +147,44 @@ def main():
         frames = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
         bgra = [torch.empty((H, W), dtype=torch.int32, device="cuda") for _ in range(2)]
         src = torch.zeros((lr, W, 4), dtype=torch.float32, device="cuda")
+        # the split present: a rank's rows encoded (device) and copied to pinned host memory
+        # on its own stream after its render (the library's copy stream)
+        pst = [torch.cuda.Stream(), torch.cuda.Stream()] if split else []
+        pdev = [torch.empty((lr, W), dtype=torch.int32, device="cuda") for _ in range(2)] if split else []
+        phost = [torch.empty((lr, W), dtype=torch.int32).pin_memory() for _ in range(2)] if split else []
+
+        def present_rows(b, rows, st_render):
+            # encode + D2H of one rank's rows (1/n of the frame); returns the encode-done event
+            ev = torch.cuda.Event()
+            ev.record(st_render)
+            pst[b].wait_event(ev)
+            wl.srgb8_encode_device(rows.data_ptr(), pdev[b].data_ptr(), lr * W, pst[b].cuda_stream)
+            enc = torch.cuda.Event()
+            enc.record(pst[b])
+            with torch.cuda.stream(pst[b]):
+                phost[b].copy_(pdev[b], non_blocking=True)
+            return enc
 
         def share(rank):
             def go(start):
                 for st in rs:
                     st.wait_event(start)
+                for st in pst:
+                    st.wait_event(start)
+                enc = [None, None]
                 for k in range(F):
                     st = rs[k & 1] if args.share_streams == 2 else rs[0]
+                    if enc[k & 1] is not None:  # the share buffer is free once its encode has read it
+                        st.wait_event(enc[k & 1])
                     r.render_rows_device(p, gather[k & 1][0].data_ptr(), T, rank, n, st.cuda_stream)
-                for st in rs:
+                    if split:
+                        enc[k & 1] = present_rows(k & 1, gather[k & 1][0], st)
+                for st in rs + pst:
                     main_s.wait_stream(st)
             return go
 
         def root(start):
-            for st in rs + [cps, asm, d2h]:
+            for st in rs + [cps, asm, d2h] + pst:
                 st.wait_event(start)
             released = [None, None]
             mapped = [None, None]  # the D2H that last read the slot's encode / frame
@@ -147,6 +193,7 @@ def main():
                 if released[b] is not None:
                     rs[b].wait_event(released[b])
                 r.render_rows_device(p, gather[b][0].data_ptr(), T, 0, n, rs[b].cuda_stream)
+                enc = present_rows(b, gather[b][0], rs[b]) if split else None
                 done = torch.cuda.Event()
                 done.record(rs[b])
                 cps.wait_event(done)
@@ -160,8 +207,10 @@ def main():
                     asm.wait_event(mapped[b])
                 wl.assemble_rows_device(gather[b].data_ptr(), frames[b].data_ptr(), W, H, T, n, asm.cuda_stream,
                                         band)
-                if not args.no_encode:
+                if not args.no_encode and not split:
                     wl.srgb8_encode_device(frames[b].data_ptr(), bgra[b].data_ptr(), W * H, asm.cuda_stream)
+                if enc is not None:  # the gather buffer is free once the split encode has read it too
+                    asm.wait_event(enc)
                 ev = torch.cuda.Event()
                 ev.record(asm)
                 released[b] = ev
@@ -174,7 +223,7 @@ def main():
                     mev = torch.cuda.Event()
                     mev.record(d2h)
                     mapped[b] = mev
-            for st in rs + [cps, asm, d2h]:
+            for st in rs + [cps, asm, d2h] + pst:
                 main_s.wait_stream(st)
 
         root(torch.cuda.Event())  # first use of the streams and buffers, untimed
@@ -188,7 +237,8 @@ def main():
                             "share_bytes": share_bytes, "projected_frame_ms": round(proj, 4),
                             "projected_speedup": round(t1 / proj, 3)}
         print(f"[root] N={n} band {band[0]}:{band[1]} rank 0 step {root_ms:.3f} ms (share + {n - 1} copies of {share_bytes / 1e6:.1f} MB "
-              f"+ assemble{'' if args.no_encode else ' + encode'}{' + D2H ' + args.map_back if mapback else ''}), "
+              f"+ assemble{'' if args.no_encode or split else ' + encode'}{' + D2H ' + args.map_back if mapback else ''}"
+              f"{'; every rank: its rows encoded + D2H (split present)' if split else ''}), "
               f"slowest other share {worst_other:.3f} ms "
               f"-> {proj:.3f} ms per frame, {t1 / proj:.2f}x", flush=True)
     print(json.dumps(res))
