@@ -2629,6 +2629,72 @@ extern "C" long long wo_jit_code_object(const char* src, const char* arch, int* 
     return (long long)code.size();
 }
 
+// The group (LDS) and private (scratch per lane) segment sizes of kernel `name` as its
+// code object states them: the first two words of its AMDHSA kernel descriptor, the
+// symbol `<name>.kd` of the ELF's symbol table.  (hipFuncGetAttribute can answer for
+// another loaded module's kernel of the same name -- a second renderer's counting
+// variant -- so kernel_info reads the code object itself.)  False if `code` is not
+// such an ELF.
+static bool kd_segment_sizes(const std::vector<char>& code, const char* name, uint32_t* group, uint32_t* priv) {
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(code.data());
+    const size_t n = code.size();
+    auto rd = [&](size_t off, size_t len, uint64_t* v) {
+        if (off > n || len > n - off) return false;
+        uint64_t x = 0;
+        for (size_t i = 0; i < len; ++i) x |= (uint64_t)b[off + i] << (8u * i);
+        *v = x;
+        return true;
+    };
+    if (n < 64 || memcmp(b, "\x7f" "ELF", 4) != 0 || b[4] != 2 || b[5] != 1) return false;  // ELF64, little-endian
+    uint64_t shoff, shentsize, shnum;
+    if (!rd(0x28, 8, &shoff) || !rd(0x3a, 2, &shentsize) || !rd(0x3c, 2, &shnum) || shentsize < 64) return false;
+    auto sh = [&](uint64_t i, size_t field, size_t len, uint64_t* v) { return rd(shoff + i * shentsize + field, len, v); };
+    const std::string want = std::string(name) + ".kd";
+    for (uint64_t i = 0; i < shnum; ++i) {
+        uint64_t type, off, size, link, entsize;
+        if (!sh(i, 4, 4, &type) || type != 2u) continue;  // SHT_SYMTAB
+        if (!sh(i, 24, 8, &off) || !sh(i, 32, 8, &size) || !sh(i, 40, 4, &link) || !sh(i, 56, 8, &entsize) ||
+            entsize < 24)
+            return false;
+        uint64_t stroff, strsize;
+        if (!sh(link, 24, 8, &stroff) || !sh(link, 32, 8, &strsize)) return false;
+        for (uint64_t k = 0; k + entsize <= size; k += entsize) {
+            uint64_t nm, shndx, value;
+            if (!rd(off + k, 4, &nm) || !rd(off + k + 6, 2, &shndx) || !rd(off + k + 8, 8, &value)) return false;
+            if (nm >= strsize || stroff + nm + want.size() + 1 > n) continue;
+            if (memcmp(b + stroff + nm, want.c_str(), want.size() + 1) != 0) continue;
+            uint64_t saddr, soff, g, p;
+            if (!sh(shndx, 16, 8, &saddr) || !sh(shndx, 24, 8, &soff) || value < saddr) return false;
+            if (!rd(soff + (value - saddr), 4, &g) || !rd(soff + (value - saddr) + 4, 4, &p)) return false;
+            *group = (uint32_t)g;
+            *priv = (uint32_t)p;
+            return true;
+        }
+    }
+    return false;
+}
+
+extern "C" int wo_jit_code_resources(const char* src, const char* arch, uint32_t* out, char* err, size_t errlen) {
+    std::vector<char> code;
+    std::string key;
+    int org = -1;
+    double sec = 0.0;
+    if (!src || !out) {
+        snprintf(err, errlen, "no source");
+        return -1;
+    }
+    if (jit_code(src, arch ? std::string(arch) : std::string("gfx950"), false, code, key, org, sec, err, errlen))
+        return -1;
+    uint32_t group = 0, priv = 0;
+    if (!kd_segment_sizes(code, "wo_jit_pathtrace", &group, &priv)) {
+        snprintf(err, errlen, "no kernel descriptor for wo_jit_pathtrace in the code object (%zu bytes)", code.size());
+        return -1;
+    }
+    out[0] = priv;
+    out[1] = group;
+    return 0;
+}
+
 static int load_jit_module(const std::vector<char>& code, hipModule_t* mod, hipFunction_t* fn, char* err,
                            size_t errlen) {
     hipError_t e = hipModuleLoadData(mod, code.data());
@@ -2678,11 +2744,20 @@ extern "C" int wo_dev_set_jit(WoDev* dev, const char* src, char* err, size_t err
     dev->jit_fn = fn;
     dev->jit_key = key;
     // its resources, read now: once the counting variant (the same kernel name in another
-    // module) is loaded, an attribute query of this function returned that one's scratch size
+    // module) is loaded, an attribute query of this function returned that one's scratch
+    // size -- and a second renderer's counting module can do the same at load time, so
+    // the scratch and LDS sizes come from this code object's kernel descriptor
     dev->jit_attr[0] = dev->jit_attr[1] = dev->jit_attr[2] = -1;
     (void)hipFuncGetAttribute(&dev->jit_attr[0], HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, fn);
     (void)hipFuncGetAttribute(&dev->jit_attr[1], HIP_FUNC_ATTRIBUTE_NUM_REGS, fn);
     (void)hipFuncGetAttribute(&dev->jit_attr[2], HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, fn);
+    {
+        uint32_t group = 0, priv = 0;
+        if (kd_segment_sizes(code, "wo_jit_pathtrace", &group, &priv)) {
+            dev->jit_attr[0] = (int)priv;
+            dev->jit_attr[2] = (int)group;
+        }
+    }
     dev->jit_src = src;
     {
         const char* m = strstr(src, "// wo_share_tiles ");

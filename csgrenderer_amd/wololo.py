@@ -147,6 +147,7 @@ SIGNATURES = {
     "wo_renderer_prepare": (c_int, [c_void_p]),
     "wo_renderer_jit_source": (c_void_p, [c_void_p]),
     "wo_jit_compile_check": (c_int, [c_char_p, c_char_p, c_char_p, c_size_t]),
+    "wo_jit_code_resources": (c_int, [c_char_p, c_char_p, POINTER(ctypes.c_uint32), c_char_p, ctypes.c_size_t]),
     "wo_jit_code_object": (ctypes.c_longlong, [c_char_p, c_char_p, POINTER(c_int), POINTER(c_double), c_char_p,
                                                c_char_p, c_size_t]),
     "wo_renderer_jit_info": (c_int, [c_void_p, POINTER(c_double)]),
@@ -541,6 +542,16 @@ def jit_code_object(src: str, arch: str = "gfx950"):
     if n < 0:
         raise WololoError(err.value.decode(errors="replace"))
     return int(n), JIT_ORIGINS[org.value], sec.value, key.value.decode()
+
+
+def jit_code_resources(src: str, arch: str = "gfx950"):
+    """(scratch bytes per lane, static LDS bytes) of the specialised kernel's code object, from
+    its kernel descriptor (wo_jit_code_resources; no GPU needed)."""
+    err = ctypes.create_string_buffer(4096)
+    out = (ctypes.c_uint32 * 2)()
+    if load().wo_jit_code_resources(src.encode(), arch.encode(), out, err, len(err)):
+        raise WololoError(err.value.decode(errors="replace"))
+    return int(out[0]), int(out[1])
 
 
 def jit_compile_check(src: str, arch: str = "gfx950") -> str:

@@ -268,6 +268,12 @@ int wo_jit_compile_check(char const* src, char const* arch, char* err, size_t er
  * Needs no GPU. */
 long long wo_jit_code_object(char const* src, char const* arch, int* origin, double* seconds, char* key_hex,
                              char* err, size_t errlen);
+/* The specialised kernel's resources as its code object states them (its AMDHSA
+ * kernel descriptor, as wo_renderer_kernel_info reports them): out[0] scratch bytes
+ * per lane (the private segment), out[1] static LDS bytes per workgroup (the group
+ * segment).  Compiles (or takes from the caches) like wo_jit_code_object.  Returns 0,
+ * or -1 (err).  Needs no GPU. */
+int wo_jit_code_resources(char const* src, char const* arch, uint32_t* out, char* err, size_t errlen);
 /* Where the renderer's specialised kernel came from (origin as above; -1: the
  * renderer does not run one) and the seconds it took (compile or load). */
 int wo_renderer_jit_info(Wo_Renderer* r, double* seconds);

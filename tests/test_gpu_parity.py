@@ -630,7 +630,14 @@ def test_kernel_info_names_the_code_object():
     assert r.kernel_info() == k, (r.kernel_info(), k)
     r2, info2 = _scene("csg32_nested", "auto")
     r2.render(info2.params(width=64, height=32, spp=1))
-    assert r2.kernel_info()["key"] != k["key"]
+    k2 = r2.kernel_info()
+    assert k2["key"] != k["key"]
+    # loaded after csg32's counting variant (a kernel of the same name in another
+    # module): its own code object's resources, as its kernel descriptor states them
+    import torch
+
+    arch = torch.cuda.get_device_properties(0).gcnArchName
+    assert (k2["scratch_bytes"], k2["lds_bytes"]) == wl.jit_code_resources(r2.jit_source(), arch), k2
     r3, info3 = _scene("rtiow_cover", "auto")
     r3.render(info3.params(width=64, height=32, spp=1))
     k3 = r3.kernel_info()

@@ -213,6 +213,21 @@ def test_persistent_code_object_cache(hostonly, tmp_path, monkeypatch):
     assert origin2 == "process" and key2 == key and n2 == n
 
 
+def test_jit_code_resources_from_the_kernel_descriptor(hostonly, monkeypatch):
+    """wo_jit_code_resources: the specialised kernel's scratch bytes per lane and static
+    LDS from its code object's AMDHSA kernel descriptor (what wo_renderer_kernel_info
+    reports; no GPU).  csg32's kernel spills nothing; its LDS is the generator's."""
+    r = wl.Renderer("res", max_nodes=4096)
+    scenes.build("csg32", r)
+    r.set_tracer("auto")
+    monkeypatch.setenv("WOLOLO_JIT_CACHE", "0")
+    scratch, lds = wl.jit_code_resources(r.jit_source(), "gfx950:sramecc+:xnack-")
+    assert scratch == 0 and 16 * 1024 < lds < 64 * 1024, (scratch, lds)
+    with pytest.raises(wl.WololoError):
+        wl.jit_code_resources("this is not HIP", "gfx950")
+    r.close()
+
+
 _RENDER_CHILD = r"""
 import json, sys, time
 sys.path.insert(0, {root!r})
