@@ -16,6 +16,11 @@
 // is wo_device_common.h; both forms agree bit-for-bit with oracle/oracle.c.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
+#include <dlfcn.h>
+#include <limits.h>
+#include <spawn.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include <stdint.h>
 #include <stdio.h>
@@ -2517,8 +2522,79 @@ static std::vector<std::string> jit_options(const std::string& arch, bool count)
     return opts;
 }
 
+// The compiler process (wo_jitc, next to this library): used when the hiprtc that
+// serves this process is not the system ROCm's -- a process that imported torch first
+// runs the library on torch's bundled HIP runtime, hiprtc and comgr (the sonames are
+// shared), and that older compiler spilled csg32_nested's kernel (12 B per lane, 3 %
+// slower).  wo_jitc links only the system hiprtc, in a
+// process of its own.  "" = compile in this process (the system hiprtc serves it, the
+// helper is missing, or WOLOLO_JITC=0).
+extern "C" char** environ;
+static const std::string& jitc_path() {
+    static const std::string path = []() -> std::string {
+        const char* env = getenv("WOLOLO_JITC");
+        if (env && *env == '0') return std::string();
+        Dl_info di;
+        char rp[PATH_MAX], rr[PATH_MAX];
+        const char* root = getenv("ROCM_PATH");
+        if (dladdr((void*)&hiprtcCompileProgram, &di) && di.dli_fname && realpath(di.dli_fname, rp) &&
+            realpath(root && *root ? root : "/opt/rocm", rr) && strncmp(rp, rr, strlen(rr)) == 0)
+            return std::string();  // the system hiprtc already
+        if (!dladdr((void*)&jitc_path, &di) || !di.dli_fname) return std::string();
+        std::string lib(di.dli_fname);
+        const size_t slash = lib.rfind('/');
+        std::string p = (slash == std::string::npos ? std::string(".") : lib.substr(0, slash)) + "/wo_jitc";
+        return access(p.c_str(), X_OK) == 0 ? p : std::string();
+    }();
+    return path;
+}
+
+// One compile through wo_jitc: the source and the code object through a private
+// temporary directory.  False: no object (the caller compiles in this process).
+static bool jitc_compile(const char* src, const std::vector<std::string>& opts, std::vector<char>& code) {
+    const char* td = getenv("TMPDIR");
+    std::string dir = std::string(td && *td ? td : "/tmp") + "/wojitc.XXXXXX";
+    if (!mkdtemp(&dir[0])) return false;
+    const std::string in = dir + "/k.hip", out = dir + "/k.co";
+    bool ok = false;
+    if (FILE* f = fopen(in.c_str(), "wb")) {
+        const size_t n = strlen(src);
+        ok = fwrite(src, 1, n, f) == n;
+        ok = (fclose(f) == 0) && ok;
+    }
+    if (ok) {
+        std::vector<char*> argv;
+        argv.push_back(const_cast<char*>(jitc_path().c_str()));
+        argv.push_back(const_cast<char*>(in.c_str()));
+        argv.push_back(const_cast<char*>(out.c_str()));
+        for (const std::string& o : opts) argv.push_back(const_cast<char*>(o.c_str()));
+        argv.push_back(nullptr);
+        pid_t pid;
+        int st = 0;
+        ok = posix_spawn(&pid, jitc_path().c_str(), nullptr, nullptr, argv.data(), environ) == 0 &&
+             waitpid(pid, &st, 0) == pid && WIFEXITED(st) && WEXITSTATUS(st) == 0;
+    }
+    if (ok) {
+        ok = false;
+        if (FILE* f = fopen(out.c_str(), "rb")) {
+            std::vector<char> buf;
+            char tmp[65536];
+            size_t n;
+            while ((n = fread(tmp, 1, sizeof tmp, f)) > 0) buf.insert(buf.end(), tmp, tmp + n);
+            fclose(f);
+            ok = buf.size() >= 4 && memcmp(buf.data(), "\x7f" "ELF", 4) == 0;
+            if (ok) code.swap(buf);
+        }
+    }
+    (void)unlink(in.c_str());
+    (void)unlink(out.c_str());
+    (void)rmdir(dir.c_str());
+    return ok;
+}
+
 static int jit_compile(const char* src, const std::string& arch, bool count, std::vector<char>& code, char* err,
                        size_t errlen) {
+    if (!jitc_path().empty() && jitc_compile(src, jit_options(arch, count), code)) return 0;
     hiprtcProgram p;
     const char* hdr_src[] = {kEmbed_wo_device_common_h, kEmbed_wo_scene_h};
     const char* hdr_names[] = {"wo_device_common.h", "wololo/wo_scene.h"};
@@ -2571,6 +2647,8 @@ static std::string jit_key(const char* src, const std::string& arch, bool count 
         return std::array<int, 3>{vmaj, vmin, vrt};
     }();
     part((const char*)ver.data(), sizeof(int) * ver.size());
+    // compiled by wo_jitc (the system hiprtc) rather than the hiprtc serving this process
+    if (!jitc_path().empty()) part("wo_jitc", 7);
     part(arch.data(), arch.size());
     for (const std::string& o : jit_options(arch, count)) part(o.data(), o.size());
     part(kEmbed_wo_device_common_h, strlen(kEmbed_wo_device_common_h));

@@ -228,6 +228,23 @@ def test_jit_code_resources_from_the_kernel_descriptor(hostonly, monkeypatch):
     r.close()
 
 
+def test_jit_compiles_with_the_system_hiprtc_under_torch(hostonly, monkeypatch):
+    """A process that imported torch first runs the library on torch's bundled ROCm
+    (HIP runtime, hiprtc, comgr: 7.0 in this image), whose compiler spilled
+    csg32_nested's kernel (2 VGPRs, 12 B per lane; 3 % slower).  The specialised
+    kernels then compile in wo_jitc, a process linked to the system ROCm's hiprtc:
+    no scratch, and a key of its own (so the two compilers' objects never mix)."""
+    import torch  # noqa: F401  (as bench.py)
+    r = wl.Renderer("nested-src", max_nodes=4096)
+    scenes.build("csg32_nested", r)
+    r.set_tracer("auto")
+    src = r.jit_source()
+    monkeypatch.setenv("WOLOLO_JIT_CACHE", "0")
+    scratch, lds = wl.jit_code_resources(src, "gfx950:sramecc+:xnack-")
+    assert scratch == 0 and lds > 0, (scratch, lds)
+    r.close()
+
+
 _RENDER_CHILD = r"""
 import json, sys, time
 sys.path.insert(0, {root!r})
