@@ -59,11 +59,11 @@ def main():
                          "(bench.py before round 5: its kernels leave the two render streams on one hardware "
                          "queue, so consecutive frames stop overlapping); 'split' = separate copy / assemble / "
                          "D2H streams (rounds 3-5)")
-    ap.add_argument("--map-back", default="bgra", choices=["split", "bgra", "float", "none"],
+    ap.add_argument("--map-back", default="bgra", choices=["split", "bgra", "direct", "float", "none"],
                     help="the presented frame's D2H: 'bgra' = rank 0 encodes and copies the whole frame after "
                          "the assembly (draw_frame's default); 'split' = every rank encodes its own rows and "
                          "copies them to the host (WOLOLO_PRESENT_SPLIT=1); 'float' adds the float frame; "
-                         "'none' skips it")
+                         "'direct' = the encode kernel writes the pinned host frame itself (no copy); 'none' skips it")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process, as bench.py sets it at N > 1 (0: leave it)")
     args = ap.parse_args()
@@ -127,6 +127,7 @@ def main():
            "d2h_gbps": {str(k): round(v[1], 2) for k, v in d2h.items()},
            "encode": not args.no_encode, "map_back": "none" if args.no_encode else args.map_back, "worlds": {}}
     split = not args.no_encode and args.map_back == "split"
+    direct = not args.no_encode and args.map_back == "direct"
     mapback = not args.no_encode and args.map_back not in ("none", "split")
     hb = [torch.empty((H, W), dtype=torch.int32).pin_memory() for _ in range(2)] if mapback else []
     hf = [torch.empty((H, W, 4), dtype=torch.float32).pin_memory() for _ in range(2)] \
@@ -208,13 +209,15 @@ def main():
                 wl.assemble_rows_device(gather[b].data_ptr(), frames[b].data_ptr(), W, H, T, n, asm.cuda_stream,
                                         band)
                 if not args.no_encode and not split:
-                    wl.srgb8_encode_device(frames[b].data_ptr(), bgra[b].data_ptr(), W * H, asm.cuda_stream)
+                    # 'direct': the encode's stores go to the pinned host frame (device-visible)
+                    wl.srgb8_encode_device(frames[b].data_ptr(), (hb[b] if direct else bgra[b]).data_ptr(), W * H,
+                                           asm.cuda_stream)
                 if enc is not None:  # the gather buffer is free once the split encode has read it too
                     asm.wait_event(enc)
                 ev = torch.cuda.Event()
                 ev.record(asm)
                 released[b] = ev
-                if mapback:
+                if mapback and not direct:
                     d2h.wait_event(ev)
                     with torch.cuda.stream(d2h):
                         hb[b].copy_(bgra[b], non_blocking=True)
